@@ -1,0 +1,321 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X Ed25519-verify / SHA-512-digest hot path.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU, RCCL)
+
+Headline (BASELINE.json metric): Ed25519 verifies/s.  Workload = BASELINE config 2:
+1M independent (32-byte msg, pk, sig) triples per GPU, all valid, `Signature::verify`
+(verify_strict) semantics; weak scaling (every rank verifies its own 1M-triple shard of
+distinct keys; no data-path collective).  A "step" is one verification pass over the 1M
+triples with inputs resident in HBM.  The per-shard verdict bitmaps are all-gathered over
+RCCL after the timed region and the gather is timed separately (it is not needed for
+correctness: every rank already holds its verdicts).
+
+Secondary leg (same JSON line, "digest"): BASELINE config 4, SHA-512[..32] of 100,000
+worker batches of 508,052 B (977 x 512-B txs, bincode WorkerMessage::Batch), hashed from a
+cycled pool of distinct batches resident in HBM.
+
+cpu_baseline: the C restatement (oracle/, "port") of dalek verify_strict on the host cores of
+the GPU box (rank 0, N = 1 only), on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Ed25519 verifies/sec at 1/2/4/8 MI355X (+% int-VALU peak); batch digest GB/s"
+
+# ---- frozen work model ------------------------------------------------------
+# W_strict: field squarings / multiplications per verify_strict in the dalek 1.0.1 serial
+# algorithm (2 decompressions, 2 small-order checks, width-5/8 NAF double-scalar-mult,
+# projective compare) + one SHA-512 block.  Converted to 32-bit-lane VALU instructions with the
+# per-op instruction counts of this build's fe_sq / fe_mul / sha512_compress (tools/count_ops.py).
+W_S, W_M, W_SHA = 1546, 1429, 1
+OPS_S, OPS_M, OPS_SHA = None, None, None  # filled from tools/op_counts.json
+# int-VALU issue peak: 64 lane-instructions / clk / CU for VOP3-class ops (v_mad_u64_u32,
+# v_mad_i64_i32, v_alignbit, v_bitop3 ...; tools/microbench/int_rates.hip) x 256 CU x 2.4 GHz
+VALU_PEAK_TOPS = 64 * 256 * 2.4e9 / 1e12      # 39.32 T lane-ops/s
+HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md (spec)
+
+CFG4_TXS, CFG4_TX_BYTES = 977, 512
+CFG4_BATCH_BYTES = 12 + CFG4_TXS * (8 + CFG4_TX_BYTES)   # 508,052
+CFG4_STRIDE = (CFG4_BATCH_BYTES + 255) & ~255
+
+
+def load_op_counts():
+    global OPS_S, OPS_M, OPS_SHA
+    with open(os.path.join(ROOT, "tools", "op_counts.json")) as f:
+        c = json.load(f)
+    OPS_S, OPS_M, OPS_SHA = c["fe_sq"], c["fe_mul"], c["sha512_block"]
+
+
+def ops_per_verify() -> float:
+    return W_S * OPS_S + W_M * OPS_M + W_SHA * OPS_SHA
+
+
+# ---- distributed ---------------------------------------------------------------------------
+def dist_setup(args):
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("WORLD_SIZE=%d but --gpus %d (launch N>1 with torch.distributed.run)" % (world, args.gpus))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def barrier(world):
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    import torch
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ---- workloads -------------------------------------------------------------------------------
+def make_cfg2(rank: int, n: int):
+    """SURVEY.md §8(d) cfg 2: seed_i = SHA-512("nw-seed"||u64le(i))[..32],
+    msg_i = SHA-512("nw-msg"||u64le(i))[..32], RFC 8032 keygen+sign (on the GPU)."""
+    from narwhal_amd import device
+    first = rank * n
+    seeds = device.derive32(b"nw-seed", first, n)
+    msgs = device.derive32(b"nw-msg", first, n)
+    pks, sigs = device.keygen_sign(seeds, msgs)
+    return msgs, pks, sigs
+
+
+def make_cfg4_pool(pool: int):
+    """`pool` distinct cfg-4 batches (bincode Batch of 977 x 512-B txs; tx = [1][u64 BE
+    counter][zeros], node/src/benchmark_client.rs:117-130), batch b's counters b*977 + j."""
+    import torch
+    tmpl = bytearray(CFG4_STRIDE)
+    tmpl[0:4] = (0).to_bytes(4, "little")
+    tmpl[4:12] = CFG4_TXS.to_bytes(8, "little")
+    pos = []
+    o = 12
+    for j in range(CFG4_TXS):
+        tmpl[o:o + 8] = CFG4_TX_BYTES.to_bytes(8, "little")
+        tmpl[o + 8] = 1
+        pos.append(o + 9)
+        o += 8 + CFG4_TX_BYTES
+    assert o == CFG4_BATCH_BYTES
+    data = torch.frombuffer(bytearray(tmpl), dtype=torch.uint8).cuda().repeat(pool)
+    view = data.view(pool, CFG4_STRIDE)
+    posj = torch.tensor(pos, dtype=torch.int64, device="cuda")
+    for b0 in range(0, pool, 1024):
+        b1 = min(pool, b0 + 1024)
+        ctr = (torch.arange(b0, b1, device="cuda", dtype=torch.int64)[:, None] * CFG4_TXS
+               + torch.arange(CFG4_TXS, device="cuda", dtype=torch.int64)[None, :])
+        for k in range(8):
+            byte = ((ctr >> (8 * (7 - k))) & 0xFF).to(torch.uint8)
+            view[b0:b1].index_copy_(1, posj + k, byte)
+    return data
+
+
+def cfg4_host_batch(b: int) -> bytes:
+    out = bytearray()
+    out += (0).to_bytes(4, "little") + CFG4_TXS.to_bytes(8, "little")
+    for j in range(CFG4_TXS):
+        out += CFG4_TX_BYTES.to_bytes(8, "little") + bytes([1]) + (b * CFG4_TXS + j).to_bytes(8, "big") + bytes(503)
+    return bytes(out)
+
+
+# ---- timing ----------------------------------------------------------------------------------
+def timed_kernel(fn, iters: int):
+    """Average duration (ms) of fn() launches measured with HIP events on torch's current
+    stream (the stream the library launches on)."""
+    import torch
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def cpu_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline_verify(msgs, pks, sigs, budget_s: float):
+    from tests.oracle_lib import load_oracle
+    orc = load_oracle()
+    th = cpu_threads()
+    m, p, s = (t.cpu().numpy() for t in (msgs, pks, sigs))
+    # calibrate on a small slice, then size the sample to ~budget_s of wall time
+    k = 2048
+    t0 = time.perf_counter()
+    v = orc.strict_many(m[:k], p[:k], s[:k], th)
+    dt = time.perf_counter() - t0
+    n = int(min(len(p), max(k, k * budget_s / max(dt, 1e-6))))
+    t0 = time.perf_counter()
+    v = orc.strict_many(m[:n], p[:n], s[:n], th)
+    dt = time.perf_counter() - t0
+    assert v.all(), "oracle rejected a valid signature"
+    return {"value": n / dt, "unit": "verifies/s", "cores": th, "kind": "port",
+            "sample": "%d of the cfg-2 triples (C restatement of dalek verify_strict, %d threads, %.1f s)" % (n, th, dt)}
+
+
+def cpu_baseline_digest(budget_s: float):
+    from tests.oracle_lib import load_oracle
+    orc = load_oracle()
+    th = cpu_threads()
+    nb = 4 * th
+    blob = b"".join(cfg4_host_batch(b) for b in range(nb))
+    data = np.frombuffer(blob, dtype=np.uint8)
+    offs = np.arange(nb + 1, dtype=np.uint64) * CFG4_BATCH_BYTES
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        orc.digest_many(data, offs, th)
+        reps += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": reps * len(blob) / dt / 1e9, "unit": "GB/s", "cores": th, "kind": "port",
+            "sample": "%d x %d cfg-4 batches (C restatement SHA-512, %d threads, %.1f s)" % (reps, nb, th, dt)}
+
+
+# ---- main ------------------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1 << 20, help="triples per GPU (cfg 2: 1M)")
+    ap.add_argument("--digest-batches", type=int, default=100000, help="cfg 4: 100k batches (0 = skip)")
+    ap.add_argument("--digest-pool", type=int, default=16384, help="distinct batches resident in HBM")
+    ap.add_argument("--digest-steps", type=int, default=1)
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU-baseline leg (0 = skip)")
+    args = ap.parse_args()
+
+    import torch
+    rank, world, local = dist_setup(args)
+    from narwhal_amd import _lib, device
+    _lib.load(device_mask=1 << local)   # the library drives the same GPU as this rank
+    load_op_counts()
+
+    # ---------------- verify leg (headline)
+    n = args.n
+    msgs, pks, sigs = make_cfg2(rank, n)
+    words = torch.empty(device.words_for(n), dtype=torch.int64, device="cuda")
+    run = lambda: device.verify(msgs, pks, sigs, strict=True, out=words)  # noqa: E731
+    for _ in range(args.warmup):
+        run()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    barrier(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    ok = bool(device.unpack_bits(words, n).all())
+    # per-launch kernel time, HIP events on the launch stream
+    kernel_ms = timed_kernel(run, max(3, args.steps))
+    # verdict all-gather over RCCL (not needed for correctness; timed separately)
+    gather_ms = None
+    if world > 1:
+        import torch.distributed as dist
+        allw = torch.empty(world * words.numel(), dtype=torch.int64, device="cuda")
+        barrier(world)
+        tg = time.perf_counter()
+        dist.all_gather_into_tensor(allw, words)
+        barrier(world)
+        gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, world)
+        ok = ok and bool(device.unpack_bits(allw, world * words.numel() * 64).all())
+    value = world * n * args.steps / dt
+    achieved_tops = n / (kernel_ms * 1e-3) * ops_per_verify() / 1e12
+
+    # ---------------- digest leg (cfg 4)
+    digest = None
+    if args.digest_batches > 0:
+        pool = min(args.digest_pool, args.digest_batches)
+        data = make_cfg4_pool(pool)
+        nb = args.digest_batches
+        # message i = pool batch (i mod pool): 100k lanes in one launch, bytes read from HBM
+        starts = (torch.arange(nb, dtype=torch.int64, device="cuda") % pool) * CFG4_STRIDE
+        ends = starts + CFG4_BATCH_BYTES
+        outs = torch.empty((nb, 32), dtype=torch.uint8, device="cuda")
+        dig = lambda: device.sha512_trunc32_ranges(data, starts, ends, out=outs)  # noqa: E731
+        dig()
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(args.digest_steps):
+            dig()
+        barrier(world)
+        ddt = max_over_ranks(time.perf_counter() - t0, world)
+        dbytes = world * nb * CFG4_BATCH_BYTES * args.digest_steps
+        o = outs[:3].cpu().numpy()
+        dok = all(o[b].tobytes() == hashlib.sha512(cfg4_host_batch(b)).digest()[:32] for b in range(3))
+        dk_ms = timed_kernel(dig, 1)
+        dk_gbs = nb * CFG4_BATCH_BYTES / (dk_ms * 1e-3) / 1e9
+        digest = {"metric": "batch digest GB/s", "value": dbytes / ddt / 1e9, "unit": "GB/s",
+                  "batches": nb, "batch_bytes": CFG4_BATCH_BYTES, "pool_distinct_batches": pool,
+                  "parity_ok": dok, "kernel": "k_sha512_digest32", "kernel_ms": dk_ms, "kernel_GBps": dk_gbs,
+                  "hbm_frac": dk_gbs / HBM_PEAK_GBS,
+                  "valu_frac": dk_gbs * 1e9 / 128 * OPS_SHA / (VALU_PEAK_TOPS * 1e12)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        cpu = cpu_baseline_verify(msgs, pks, sigs, args.cpu_budget)
+        if digest is not None:
+            digest["cpu_baseline"] = cpu_baseline_digest(args.cpu_budget / 2)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic: SHA-512-derived seeds/messages, RFC 8032 keygen+sign on the GPU (SURVEY.md §8(d) cfg 2)",
+            "config": {"workload": "cfg2: %d independent (32-B msg, pk, sig) triples per GPU, all valid, "
+                                   "verify_strict" % n,
+                       "global_batch": world * n, "parallelism": "shard%d" % world,
+                       "verdicts_ok": ok, "verdict_allgather_ms": gather_ms,
+                       "allgather_needed": False},
+            "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
+                         "frac": achieved_tops / VALU_PEAK_TOPS, "traffic": None,
+                         "kernel": "k_verify", "kernel_ms": kernel_ms,
+                         "ops_per_verify": ops_per_verify(),
+                         "work_model": "%d S + %d M + %d SHA-512 block per verify (dalek op model) x "
+                                       "(%d, %d, %d) VALU lane-ops" % (W_S, W_M, W_SHA, OPS_S, OPS_M, OPS_SHA)},
+            "cpu_baseline": cpu,
+            "digest": digest,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

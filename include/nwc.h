@@ -1,0 +1,110 @@
+/*
+ * nwc.h -- C ABI of the MI355X-native Narwhal signature-and-digest hot path (libnwc.so).
+ *
+ * This is the drop-in boundary: the reference's `crypto` crate keeps its Rust API and calls
+ * these entry points through a thin FFI shim.  Every entry point names the
+ * reference interface it replaces (paths under /root/reference).
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; all buffers are caller-owned.  Host entry points take
+ *     host memory; `nwc_dev_*` entry points take device (HBM) pointers and a hipStream_t
+ *     passed as void* (NULL = the library's own stream) and are asynchronous on it.
+ *   - Single verdicts: 0 = valid (Rust `Ok(())`), 1 = invalid (`Err(CryptoError)`),
+ *     < 0 = runtime/device/argument error (never reported as "invalid"; the Rust shim panics).
+ *   - Batch calls return 0 on success (< 0 on error) and fill bitmaps: bit i of a bitmap is
+ *     byte i/8, bit i%8 (LSB first); 1 = valid for verdict bitmaps, 1 = bad for bad-vote bitmaps.
+ *     Device bitmaps are arrays of uint64_t words with the same bit order.
+ *   - Messages at the crypto surface are always 32-byte `Digest`s (crypto/src/lib.rs:203,214).
+ *   - Thread-safe and reentrant (tokio tasks call concurrently: worker/src/worker.rs:182,227).
+ */
+#ifndef NWC_H
+#define NWC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NWC_OK 0
+#define NWC_INVALID 1
+#define NWC_ERR_DEVICE (-1)
+#define NWC_ERR_ARG (-2)
+#define NWC_ERR_NOT_INIT (-3)
+#define NWC_ERR_NO_DEVICE (-4)
+
+/* ---- lifecycle ------------------------------------------------------------------------ */
+/* Node start-up hook (node/src/main.rs:69-134).  device_mask: bit d = use HIP device d
+ * (0 = device 0).  Builds the basepoint table on each device.  Idempotent. */
+int nwc_init(uint32_t device_mask);
+void nwc_shutdown(void);
+/* Text of the last error on the calling thread ("" if none). */
+const char* nwc_last_error(void);
+/* ABI version (major << 16 | minor). */
+int nwc_version(void);
+/* Number of devices initialised. */
+int nwc_device_count(void);
+
+/* ---- verification ----------------------------------------------------------------------- */
+/* crypto::Signature::verify -> dalek verify_strict.  Replaces crypto/src/lib.rs:200-204
+ * (called from primary/src/messages.rs:63-66 Header::verify and :138-141 Vote::verify). */
+int nwc_verify_strict(const uint8_t msg32[32], const uint8_t pk[32], const uint8_t sig[64]);
+
+/* crypto::Signature::verify_batch(digest, votes).  Replaces crypto/src/lib.rs:206-219
+ * (called from primary/src/messages.rs:214 Certificate::verify).  Votes are n (pk, sig) pairs
+ * laid out as pks[32*n], sigs[64*n].  n == 0 -> valid.  bad_bitmap (nullable, ceil(n/8)
+ * bytes) receives the exact set of failing votes (the per-signature leaf). */
+int nwc_verify_batch(const uint8_t msg32[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
+                     uint8_t* bad_bitmap);
+
+/* n independent Signature::verify calls (BASELINE configs 2 and 5). */
+int nwc_verify_strict_many(const uint8_t* msgs32, const uint8_t* pks, const uint8_t* sigs, size_t n,
+                           uint8_t* verdict_bitmap);
+
+/* m certificates (BASELINE config 3): certificate c has digest digests[32c] and votes
+ * [offsets[c], offsets[c+1]) of pks/sigs; offsets[0] must be 0.  cert_ok_bitmap: m bits,
+ * bad_vote_bitmap (nullable): offsets[m] bits. */
+int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
+                          const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap,
+                          uint8_t* bad_vote_bitmap);
+
+/* Committee key cache (config/src/lib.rs:154-156 Committee).  Optional: verdicts never
+ * depend on it. */
+int nwc_set_committee(const uint8_t* pks, size_t n);
+
+/* ---- digests -------------------------------------------------------------------------- */
+/* Sha512::digest(bytes)[..32] -- worker/src/processor.rs:38 and crypto's `Hash for &[u8]`
+ * (crypto/src/tests/crypto_tests.rs:8-12). */
+int nwc_digest32(const uint8_t* data, size_t len, uint8_t out32[32]);
+/* n messages data[offsets[i] .. offsets[i+1]) -> out32[32*i]. */
+int nwc_sha512_trunc32_many(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32);
+
+/* ---- device-resident variants (inputs already in HBM) ---------------------------------- */
+/* strict != 0: verify_strict semantics; strict == 0: batch-leaf semantics.  msg_index
+ * (nullable, device u32[n]) selects the digest of equation i; otherwise digest i*msg_stride. */
+int nwc_dev_verify(const void* d_msgs, const void* d_msg_index, uint64_t msg_stride,
+                   const void* d_pks, const void* d_sigs, uint64_t n, int strict,
+                   void* d_verdict_words, void* stream);
+/* Per-certificate AND of leaf verdict words (d_offsets: device u32[m+1]). */
+int nwc_dev_cert_reduce(const void* d_leaf_words, const void* d_offsets, uint64_t m, uint64_t nvotes,
+                        void* d_cert_words, void* d_bad_words, void* stream);
+int nwc_dev_sha512_trunc32(const void* d_data, const void* d_offsets, uint64_t n, void* d_out32,
+                           void* stream);
+/* Same, message i = d_data[d_starts[i] .. d_ends[i]) (device u64 arrays): any layout, e.g. a
+ * pool of resident batches hashed repeatedly.  Starts 16-byte aligned take the fast path. */
+int nwc_dev_sha512_trunc32_ranges(const void* d_data, const void* d_starts, const void* d_ends, uint64_t n,
+                                  void* d_out32, void* stream);
+/* Synthetic workload generation (BASELINE configs 2/3/5): out_i = SHA-512(tag||u64le(first+i))[..32]
+ * and RFC 8032 keygen+sign of (seed_i, msg_i). */
+int nwc_dev_derive32(const uint8_t* tag, int taglen, uint64_t first, uint64_t n, void* d_out,
+                     void* stream);
+int nwc_dev_keygen_sign(const void* d_seeds, const void* d_msgs, uint64_t n, void* d_pks,
+                        void* d_sigs, void* stream);
+/* Select the HIP device used by nwc_dev_* on the calling thread (index into the init mask). */
+int nwc_dev_set_device(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NWC_H */

@@ -1,0 +1,145 @@
+// Edwards25519 group arithmetic on top of fe25519.h (one point per lane).
+//
+// Coordinates (twisted Edwards, a = -1, d = -121665/121666):
+//   ge_p2     (X:Y:Z)            x = X/Z, y = Y/Z
+//   ge_p3     (X:Y:Z:T)          extended, T = XY/Z
+//   ge_p1p1   (X:Y:Z:T)          "completed": x = X/Z, y = Y/T (output of add/dbl)
+//   ge_cached (Y+X, Y-X, Z, 2dT) for the variable-base table
+//   ge_niels  (y+x, y-x, 2dxy)   affine, for the fixed basepoint table
+// Formulas: add-2008-hwcd-3 (unified addition) and dbl-2008-hwcd from the Explicit-Formulas
+// Database; both are complete on Ed25519 because d is a non-square.  The results are group
+// elements, so the verdicts are independent of the chosen formulas (dalek compares points,
+// SURVEY.md A.3 step 5).
+#pragma once
+#include "fe25519.h"
+#include "consts.h"
+
+namespace nwc {
+
+struct ge_p2 { fe X, Y, Z; };
+struct ge_p3 { fe X, Y, Z, T; };
+struct ge_p1p1 { fe X, Y, Z, T; };
+struct ge_cached { fe YpX, YmX, Z, T2d; };
+struct ge_niels { fe ypx, ymx, xy2d; };
+
+FE_DEV ge_p3 ge_p3_identity() { ge_p3 r; r.X = fe_zero(); r.Y = fe_one(); r.Z = fe_one(); r.T = fe_zero(); return r; }
+FE_DEV ge_cached ge_cached_identity() {
+  ge_cached r; r.YpX = fe_one(); r.YmX = fe_one(); r.Z = fe_one(); r.T2d = fe_zero(); return r;
+}
+FE_DEV ge_niels ge_niels_identity() { ge_niels r; r.ypx = fe_one(); r.ymx = fe_one(); r.xy2d = fe_zero(); return r; }
+
+FE_DEV ge_p2 ge_p1p1_to_p2(const ge_p1p1& p) {
+  ge_p2 r; r.X = fe_mul(p.X, p.T); r.Y = fe_mul(p.Y, p.Z); r.Z = fe_mul(p.Z, p.T); return r;
+}
+FE_DEV ge_p3 ge_p1p1_to_p3(const ge_p1p1& p) {
+  ge_p3 r; r.X = fe_mul(p.X, p.T); r.Y = fe_mul(p.Y, p.Z); r.Z = fe_mul(p.Z, p.T); r.T = fe_mul(p.X, p.Y); return r;
+}
+FE_DEV ge_p2 ge_p3_to_p2(const ge_p3& p) { ge_p2 r; r.X = p.X; r.Y = p.Y; r.Z = p.Z; return r; }
+FE_DEV ge_cached ge_p3_to_cached(const ge_p3& p) {
+  ge_cached r; r.YpX = fe_add(p.Y, p.X); r.YmX = fe_sub(p.Y, p.X); r.Z = p.Z; r.T2d = fe_mul(p.T, FE_D2); return r;
+}
+FE_DEV ge_p3 ge_p3_neg(const ge_p3& p) { ge_p3 r = p; r.X = fe_neg(p.X); r.T = fe_neg(p.T); return r; }
+
+// dbl-2008-hwcd, a = -1: from (X:Y:Z) only (T not needed).  4 squarings.
+FE_DEV ge_p1p1 ge_p2_dbl(const ge_p2& p) {
+  ge_p1p1 r;
+  fe xx = fe_sq(p.X);
+  fe yy = fe_sq(p.Y);
+  fe b = fe_sq2(p.Z);
+  fe a = fe_sq(fe_add(p.X, p.Y));
+  r.Y = fe_add(yy, xx);          // -H
+  r.Z = fe_sub(yy, xx);          //  G
+  r.X = fe_sub(a, r.Y);          //  E
+  r.T = fe_sub(b, r.Z);          // -F
+  return r;
+}
+
+// p + q, q cached.  4 multiplications.
+FE_DEV ge_p1p1 ge_add_cached(const ge_p3& p, const ge_cached& q) {
+  ge_p1p1 r;
+  fe pp = fe_mul(fe_add(p.Y, p.X), q.YpX);
+  fe mm = fe_mul(fe_sub(p.Y, p.X), q.YmX);
+  fe tt = fe_mul(p.T, q.T2d);
+  fe zz = fe_mul(p.Z, q.Z);
+  fe zz2 = fe_add(zz, zz);
+  r.X = fe_sub(pp, mm);
+  r.Y = fe_add(pp, mm);
+  r.Z = fe_add(zz2, tt);
+  r.T = fe_sub(zz2, tt);
+  return r;
+}
+
+// p + q, q affine niels.  3 multiplications.
+FE_DEV ge_p1p1 ge_add_niels(const ge_p3& p, const ge_niels& q) {
+  ge_p1p1 r;
+  fe pp = fe_mul(fe_add(p.Y, p.X), q.ypx);
+  fe mm = fe_mul(fe_sub(p.Y, p.X), q.ymx);
+  fe tt = fe_mul(p.T, q.xy2d);
+  fe zz2 = fe_add(p.Z, p.Z);
+  r.X = fe_sub(pp, mm);
+  r.Y = fe_add(pp, mm);
+  r.Z = fe_add(zz2, tt);
+  r.T = fe_sub(zz2, tt);
+  return r;
+}
+
+// Conditional negation of a table entry: -(x, y) = (-x, y) swaps Y+X <-> Y-X and negates T.
+FE_DEV ge_cached ge_cached_cneg(const ge_cached& q, bool neg) {
+  ge_cached r;
+  r.YpX = fe_select(q.YpX, q.YmX, neg);
+  r.YmX = fe_select(q.YmX, q.YpX, neg);
+  r.Z = q.Z;
+  r.T2d = fe_select(q.T2d, fe_neg(q.T2d), neg);
+  return r;
+}
+FE_DEV ge_niels ge_niels_cneg(const ge_niels& q, bool neg) {
+  ge_niels r;
+  r.ypx = fe_select(q.ypx, q.ymx, neg);
+  r.ymx = fe_select(q.ymx, q.ypx, neg);
+  r.xy2d = fe_select(q.xy2d, fe_neg(q.xy2d), neg);
+  return r;
+}
+
+// curve25519-dalek CompressedEdwardsY::decompress:
+//   y = low 255 bits (y >= p accepted), u = y^2 - 1, v = d y^2 + 1, (ok, x) = sqrt_ratio_i(u, v),
+//   x := -x if the sign bit is set -- even when x == 0.
+// Also returns the canonical y words (for the small-order test and the caller's use).
+FE_DEV bool ge_decompress(ge_p3& out, const u32 w[8], u32 ycanon[8]) {
+  fe y = fe_from_words(w);
+  fe one = fe_one();
+  fe yy = fe_sq(y);
+  fe u = fe_sub(yy, one);
+  fe v = fe_add(fe_mul(yy, FE_D), one);
+  fe v3 = fe_mul(fe_sq(v), v);
+  fe v7 = fe_mul(fe_sq(v3), v);
+  fe r = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(u, v7)));
+  fe check = fe_mul(v, fe_sq(r));
+  const bool correct = fe_equal(check, u);
+  const bool flipped = fe_is_zero(fe_add(check, u));
+  const bool flipped_i = fe_is_zero(fe_add(check, fe_mul(u, FE_SQRTM1)));
+  r = fe_select(r, fe_mul(r, FE_SQRTM1), flipped || flipped_i);
+  r = fe_select(r, fe_neg(r), fe_is_negative(r));
+  const bool sign = (w[7] >> 31) & 1;
+  fe x = fe_select(r, fe_neg(r), sign);
+  out.X = x;
+  out.Y = y;
+  out.Z = one;
+  out.T = fe_mul(x, y);
+  fe_to_words(y, ycanon);
+  return correct || flipped;
+}
+
+// A decompressed point is small-order iff its y is one of the five y-coordinates of E[8]
+// (0, 1, -1, +-y8): every such y decodes, and E[8] has exactly these y values.  Equivalent
+// to dalek's `mul_by_cofactor().is_identity()` for decoded points.
+FE_DEV bool ycanon_is_small_order(const u32 y[8]) {
+  bool so = false;
+  _Pragma("unroll") for (int k = 0; k < 5; ++k) {
+    u32 diff = 0;
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) diff |= y[i] ^ SMALL_ORDER_Y[k][i];
+    so = so || (diff == 0);
+  }
+  return so;
+}
+
+}  // namespace nwc

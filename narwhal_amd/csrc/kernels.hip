@@ -1,0 +1,433 @@
+// HIP kernels of the Narwhal signature-and-digest hot path for gfx950 (MI355X).
+//
+//   k_build_base_table   i*B, i = 0..128, as affine Niels points (run once at nwc_init)
+//   k_verify             one Ed25519 verification equation per lane:
+//                          mode STRICT = dalek verify_strict      (crypto/src/lib.rs:200-204)
+//                          mode LEAF   = batch leaf, A.5           (crypto/src/lib.rs:206-219)
+//                        verdicts leave as a 64-bit ballot per wave (bit i = lane i valid)
+//   k_cert_reduce        per-certificate AND of leaf bits + bad-vote bitmap
+//   k_sha512_digest32    Sha512::digest(batch)[..32] per message (worker/src/processor.rs:38)
+//   k_keygen_sign        synthetic (pk, sig) generation (RFC 8032 == dalek sign) for workloads
+//
+// Verification per lane:
+//   1. s < l                                       (A.1)
+//   2. decompress A and R (dalek quirks)           (A.2)
+//   3. STRICT: reject small-order A or R           (A.3 step 3)
+//   4. k = SHA-512(R_bytes || A_bytes || M) mod l  (A.3 step 4, raw input bytes)
+//   5. R' = k(-A) + sB with a uniform fixed-window ladder: 63 x 4 shared doublings, a signed
+//      radix-16 digit of k every 4 bits (9-entry per-lane table of -A multiples) and a signed
+//      radix-256 digit of s every 8 bits (129-entry basepoint table in LDS).  Fixed windows keep
+//      every lane of a wave on the same add schedule (a w-NAF would make nearly every bit
+//      position an add for some lane of 64).
+//   6. valid iff R' == R as group elements (X_R' = x_R Z_R', Y_R' = y_R Z_R')  (A.3 step 5)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "fe25519.h"
+#include "ge25519.h"
+#include "sc25519.h"
+#include "sha512.h"
+
+namespace nwc {
+
+// ------------------------------------------------------------------------------- helpers
+__device__ __forceinline__ void load_words8(const uint8_t* p, u32 w[8]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+// Affine Niels form of an extended point (one inversion; setup/generation only).
+__device__ ge_niels ge_p3_to_niels(const ge_p3& p) {
+  fe zi = fe_invert(p.Z);
+  fe x = fe_mul(p.X, zi), y = fe_mul(p.Y, zi);
+  ge_niels r;
+  r.ypx = fe_add(y, x);
+  r.ymx = fe_sub(y, x);
+  r.xy2d = fe_mul(fe_mul(x, y), FE_D2);
+  return r;
+}
+
+__device__ void ge_p3_compress(const ge_p3& p, u32 out[8]) {
+  fe zi = fe_invert(p.Z);
+  fe x = fe_mul(p.X, zi), y = fe_mul(p.Y, zi);
+  fe_to_words(y, out);
+  out[7] |= (u32)fe_is_negative(x) << 31;
+}
+
+__device__ ge_p3 ge_base_point() {
+  ge_p3 b;
+  b.X = FE_BASE_X; b.Y = FE_BASE_Y; b.Z = fe_one(); b.T = fe_mul(FE_BASE_X, FE_BASE_Y);
+  return b;
+}
+
+// SHA-512 of one short message (len <= 111 bytes) given as little-endian words.
+__device__ void sha512_one_block(const u32* words, int len, u32 digest_le[16]) {
+  uint64_t w[16];
+  _Pragma("unroll") for (int i = 0; i < 16; ++i) {
+    u32 lo = (2 * i < 28) ? words[2 * i] : 0u;
+    u32 hi = (2 * i + 1 < 28) ? words[2 * i + 1] : 0u;
+    // mask bytes beyond len, append 0x80
+    u32 bl = 0, bh = 0;
+    _Pragma("unroll") for (int b = 0; b < 4; ++b) {
+      int ilo = 8 * i + b, ihi = 8 * i + 4 + b;
+      u32 vlo = (ilo < len) ? ((lo >> (8 * b)) & 0xFF) : (ilo == len ? 0x80u : 0u);
+      u32 vhi = (ihi < len) ? ((hi >> (8 * b)) & 0xFF) : (ihi == len ? 0x80u : 0u);
+      bl |= vlo << (8 * b);
+      bh |= vhi << (8 * b);
+    }
+    w[i] = be64_from_le32(bl, bh);
+  }
+  w[15] = (uint64_t)len * 8;
+  uint64_t st[8];
+  sha512_init_state(st);
+  sha512_compress(st, w);
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    digest_le[2 * i] = __builtin_bswap32((u32)(st[i] >> 32));
+    digest_le[2 * i + 1] = __builtin_bswap32((u32)st[i]);
+  }
+}
+
+// ------------------------------------------------------------------------------- base table
+// table[i] = i*B (i = 0..128) in affine Niels form.  One lane per entry.
+__global__ void k_build_base_table(ge_niels* table) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > 128) return;
+  ge_p3 b = ge_base_point();
+  ge_cached bc = ge_p3_to_cached(b);
+  ge_p3 acc = ge_p3_identity();
+  for (int bit = 7; bit >= 0; --bit) {
+    acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
+    if ((i >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, bc));
+  }
+  table[i] = ge_p3_to_niels(acc);
+}
+
+// ------------------------------------------------------------------------------- ladder
+// R' = k*P + s*B where P is given by its 9-entry cached table tab[0..8] = {O, P, 2P, .., 8P}.
+// kd: radix-16 digits of k (nibble d+8), sd: radix-256 digits of s (byte d+128).
+__device__ __noinline__ ge_p2 double_scalarmult(const ge_cached* tab, u32 kd[8], u32 sd[8],
+                                                const ge_niels* sB) {
+  ge_p3 acc = ge_p3_identity();
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int w = 63; w >= 0; --w) {
+    if (w != 63) {
+      ge_p2 p2 = ge_p1p1_to_p2(t);
+      t = ge_p2_dbl(p2);
+      p2 = ge_p1p1_to_p2(t);
+      t = ge_p2_dbl(p2);
+      p2 = ge_p1p1_to_p2(t);
+      t = ge_p2_dbl(p2);
+      p2 = ge_p1p1_to_p2(t);
+      t = ge_p2_dbl(p2);
+      acc = ge_p1p1_to_p3(t);
+    }
+    // k digit: top nibble of kd
+    const i32 dk = (i32)(kd[7] >> 28) - 8;
+    digits_shl(kd, 4);
+    const int ak = dk < 0 ? -dk : dk;
+    ge_cached e = tab[ak];
+    t = ge_add_cached(acc, ge_cached_cneg(e, dk < 0));
+    if ((w & 1) == 0) {
+      const i32 ds = (i32)(sd[7] >> 24) - 128;
+      digits_shl(sd, 8);
+      const int as = ds < 0 ? -ds : ds;
+      ge_niels nb = sB[as];
+      acc = ge_p1p1_to_p3(t);
+      t = ge_add_niels(acc, ge_niels_cneg(nb, ds < 0));
+    }
+  }
+  return ge_p1p1_to_p2(t);
+}
+
+__device__ __noinline__ bool decompress_point(ge_p3& out, const u32 w[8], u32 ycanon[8]) {
+  return ge_decompress(out, w, ycanon);
+}
+
+// One verification equation.  Returns the verdict bit.
+__device__ bool verify_one(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict,
+                           const ge_niels* sB) {
+  u32 rw[8], sw[8];
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) { rw[i] = sigw[i]; sw[i] = sigw[8 + i]; }
+  const bool s_ok = sc_lt_l(sw);
+
+  ge_p3 A, R;
+  u32 ya[8], yr[8];
+  const bool a_ok = decompress_point(A, aw, ya);
+  const bool r_ok = decompress_point(R, rw, yr);
+  const bool small = strict && (ycanon_is_small_order(ya) || ycanon_is_small_order(yr));
+
+  // k = SHA-512(R || A || M) mod l, over the raw input bytes
+  uint64_t w[16];
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) {
+    w[i] = be64_from_le32(rw[2 * i], rw[2 * i + 1]);
+    w[4 + i] = be64_from_le32(aw[2 * i], aw[2 * i + 1]);
+    w[8 + i] = be64_from_le32(mw[2 * i], mw[2 * i + 1]);
+  }
+  w[12] = 0x8000000000000000ULL; w[13] = 0; w[14] = 0; w[15] = 96 * 8;
+  uint64_t st[8];
+  sha512_init_state(st);
+  sha512_compress(st, w);
+  u32 hw[16];
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    hw[2 * i] = __builtin_bswap32((u32)(st[i] >> 32));
+    hw[2 * i + 1] = __builtin_bswap32((u32)st[i]);
+  }
+  u32 kw[8];
+  sc_reduce512(hw, kw);
+
+  // table of -A multiples: tab[j] = j * (-A)
+  ge_cached tab[9];
+  ge_p3 na = ge_p3_neg(A);
+  tab[0] = ge_cached_identity();
+  tab[1] = ge_p3_to_cached(na);
+  ge_p3 pj = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(na)));
+  tab[2] = ge_p3_to_cached(pj);
+#pragma unroll 1
+  for (int j = 3; j <= 8; ++j) {
+    pj = ge_p1p1_to_p3(ge_add_cached(pj, tab[1]));
+    tab[j] = ge_p3_to_cached(pj);
+  }
+  u32 kd[8], sd[8];
+  sc_recode_radix16(kw, kd);
+  sc_recode_radix256(sw, sd);
+  ge_p2 rp = double_scalarmult(tab, kd, sd, sB);
+
+  // R' == R  <=>  X' == x_R Z'  and  Y' == y_R Z'   (R affine: Z = 1)
+  const bool eq = fe_is_zero(fe_sub(rp.X, fe_mul(R.X, rp.Z))) && fe_is_zero(fe_sub(rp.Y, fe_mul(R.Y, rp.Z)));
+  return s_ok && a_ok && r_ok && !small && eq;
+}
+
+// ------------------------------------------------------------------------------- verify
+// n equations; equation i uses msgs[32 * (msg_index ? msg_index[i] : i * msg_stride)], pks[32 i],
+// sigs[64 i] (msg_stride 0 broadcasts one digest: Signature::verify_batch, crypto/src/lib.rs:214).
+// out_bits[i / 64] bit (i % 64) = verdict.  Grid-stride over 256-lane tiles.
+__global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ msgs,
+                                                const uint32_t* __restrict__ msg_index, uint64_t msg_stride,
+                                                const uint8_t* __restrict__ pks,
+                                                const uint8_t* __restrict__ sigs,
+                                                uint64_t* __restrict__ out_bits, uint64_t n,
+                                                int strict, const ge_niels* __restrict__ base_table) {
+  __shared__ ge_niels sB[129];
+  for (int i = threadIdx.x; i < 129 * 30; i += blockDim.x)
+    reinterpret_cast<i32*>(sB)[i] = reinterpret_cast<const i32*>(base_table)[i];
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+    const uint64_t i = base + threadIdx.x;
+    const bool active = i < n;
+    const uint64_t ii = active ? i : 0;
+    u32 mw[8], aw[8], sgw[16];
+    const uint64_t mi = msg_index ? (uint64_t)msg_index[ii] : ii * msg_stride;
+    load_words8(msgs + 32 * mi, mw);
+    load_words8(pks + 32 * ii, aw);
+    load_words8(sigs + 64 * ii, sgw);
+    load_words8(sigs + 64 * ii + 32, sgw + 8);
+    bool v = verify_one(mw, aw, sgw, strict != 0, sB) && active;
+    const uint64_t ballot = __ballot(v);
+    if ((threadIdx.x & 63) == 0 && base + (threadIdx.x & ~63u) < n) out_bits[(base + threadIdx.x) >> 6] = ballot;
+  }
+}
+
+// ------------------------------------------------------------------------------- certificates
+// cert c owns votes [voffs[c], voffs[c+1]); cert_ok bit c = AND of its leaf bits (empty -> 1);
+// bad_bits = NOT leaf bits over valid vote indices.
+__global__ void k_cert_reduce(const uint64_t* __restrict__ leaf_bits, const uint32_t* __restrict__ voffs,
+                              uint64_t m, uint64_t nvotes, uint64_t* __restrict__ cert_bits,
+                              uint64_t* __restrict__ bad_bits) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool ok = true;
+  if (c < m) {
+    const uint32_t a = voffs[c], b = voffs[c + 1];
+    for (uint32_t v = a; v < b; ++v) ok = ok && ((leaf_bits[v >> 6] >> (v & 63)) & 1);
+  }
+  const uint64_t ballot = __ballot(ok && c < m);
+  if ((threadIdx.x & 63) == 0 && c < m) cert_bits[c >> 6] = ballot;
+  // bad bits: one word per thread
+  const uint64_t words = (nvotes + 63) / 64;
+  if (bad_bits && c < words) {
+    uint64_t wv = ~leaf_bits[c];
+    const uint64_t lo = c * 64;
+    if (lo + 64 > nvotes) wv &= (nvotes - lo >= 64) ? ~0ull : ((1ull << (nvotes - lo)) - 1);
+    bad_bits[c] = wv;
+  }
+}
+
+// ------------------------------------------------------------------------------- SHA-512 digests
+// digest32 of message i = data[offsets[i] .. (ends ? ends[i] : offsets[i+1])).  One lane per
+// message; a 16-byte-aligned start takes the dwordx4 path.
+__global__ __launch_bounds__(256) void k_sha512_digest32(const uint8_t* __restrict__ data,
+                                                         const uint64_t* __restrict__ offsets,
+                                                         const uint64_t* __restrict__ ends,
+                                                         uint64_t n, uint8_t* __restrict__ out32) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t start = offsets[i];
+  const uint64_t len = (ends ? ends[i] : offsets[i + 1]) - start;
+  const uint8_t* p = data + start;
+  uint64_t st[8];
+  sha512_init_state(st);
+  const uint64_t nfull = len >> 7;
+  uint64_t w[16];
+  if ((start & 15) == 0) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll 1
+    for (uint64_t b = 0; b < nfull; ++b) {
+      uint4 v[8];
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] = q[8 * b + j];
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) {
+        w[2 * j] = be64_from_le32(v[j].x, v[j].y);
+        w[2 * j + 1] = be64_from_le32(v[j].z, v[j].w);
+      }
+      sha512_compress(st, w);
+    }
+  } else {
+#pragma unroll 1
+    for (uint64_t b = 0; b < nfull; ++b) {
+      _Pragma("unroll") for (int j = 0; j < 16; ++j) {
+        uint64_t x = 0;
+        _Pragma("unroll") for (int k = 0; k < 8; ++k) x = (x << 8) | p[128 * b + 8 * j + k];
+        w[j] = x;
+      }
+      sha512_compress(st, w);
+    }
+  }
+  // tail: rem bytes + 0x80 + zeros + 128-bit big-endian bit length (1 or 2 blocks)
+  const uint32_t rem = (uint32_t)(len - (nfull << 7));
+  const uint8_t* t = p + (nfull << 7);
+  const int nblk = rem <= 111 ? 1 : 2;
+#pragma unroll 1
+  for (int blk = 0; blk < nblk; ++blk) {
+    _Pragma("unroll") for (int j = 0; j < 16; ++j) {
+      uint64_t x = 0;
+      _Pragma("unroll") for (int k = 0; k < 8; ++k) {
+        const uint32_t idx = (uint32_t)(128 * blk + 8 * j + k);
+        const uint32_t byte = idx < rem ? t[idx] : (idx == rem ? 0x80u : 0u);
+        x = (x << 8) | byte;
+      }
+      w[j] = x;
+    }
+    if (blk == nblk - 1) { w[14] = len >> 61; w[15] = len << 3; }
+    sha512_compress(st, w);
+  }
+  uint32_t* o = reinterpret_cast<uint32_t*>(out32 + 32 * i);
+  _Pragma("unroll") for (int j = 0; j < 4; ++j) {
+    o[2 * j] = __builtin_bswap32((u32)(st[j] >> 32));
+    o[2 * j + 1] = __builtin_bswap32((u32)st[j]);
+  }
+}
+
+// ------------------------------------------------------------------------------- keygen + sign
+// Fixed-base scalar multiplication by a reduced scalar (< l) with the LDS base table.
+__device__ __noinline__ ge_p3 base_scalarmult(const u32 a[8], const ge_niels* sB) {
+  u32 sd[8];
+  sc_recode_radix256(a, sd);
+  ge_p3 acc = ge_p3_identity();
+#pragma unroll 1
+  for (int w = 31; w >= 0; --w) {
+    if (w != 31) {
+      ge_p2 p2 = ge_p3_to_p2(acc);
+      ge_p1p1 t;
+#pragma unroll 1
+      for (int k = 0; k < 7; ++k) { t = ge_p2_dbl(p2); p2 = ge_p1p1_to_p2(t); }
+      t = ge_p2_dbl(p2);
+      acc = ge_p1p1_to_p3(t);
+    }
+    const i32 ds = (i32)(sd[7] >> 24) - 128;
+    digits_shl(sd, 8);
+    const int as = ds < 0 ? -ds : ds;
+    acc = ge_p1p1_to_p3(ge_add_niels(acc, ge_niels_cneg(sB[as], ds < 0)));
+  }
+  return acc;
+}
+
+// Lane i: seed_i (32 B) and msg_i (32 B) -> pk_i (32 B), sig_i (64 B).  RFC 8032 / dalek:
+//   h = SHA-512(seed); a = clamp(h[0..32]); A = aB; r = SHA-512(h[32..64] || M) mod l;
+//   R = rB; k = SHA-512(R || A || M) mod l; s = r + k a mod l.
+__global__ __launch_bounds__(256) void k_keygen_sign(const uint8_t* __restrict__ seeds,
+                                                     const uint8_t* __restrict__ msgs, uint64_t n,
+                                                     uint8_t* __restrict__ pks, uint8_t* __restrict__ sigs,
+                                                     const ge_niels* __restrict__ base_table) {
+  __shared__ ge_niels sB[129];
+  for (int i = threadIdx.x; i < 129 * 30; i += blockDim.x)
+    reinterpret_cast<i32*>(sB)[i] = reinterpret_cast<const i32*>(base_table)[i];
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  u32 seed[8], m[8];
+  load_words8(seeds + 32 * i, seed);
+  load_words8(msgs + 32 * i, m);
+  u32 sbuf[28];
+  _Pragma("unroll") for (int j = 0; j < 28; ++j) sbuf[j] = j < 8 ? seed[j] : 0u;
+  u32 h[16];
+  sha512_one_block(sbuf, 32, h);
+  u32 a[8];
+  _Pragma("unroll") for (int j = 0; j < 8; ++j) a[j] = h[j];
+  a[0] &= 0xFFFFFFF8u; a[7] &= 0x7FFFFFFFu; a[7] |= 0x40000000u;
+  // a mod l (aB = (a mod l) B since B has order l)
+  u32 wide[16];
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) wide[j] = j < 8 ? a[j] : 0u;
+  u32 ar[8];
+  sc_reduce512(wide, ar);
+  u32 pk[8];
+  ge_p3_compress(base_scalarmult(ar, sB), pk);
+  u32 buf[28];
+  _Pragma("unroll") for (int j = 0; j < 28; ++j) buf[j] = 0;
+  _Pragma("unroll") for (int j = 0; j < 8; ++j) { buf[j] = h[8 + j]; buf[8 + j] = m[j]; }
+  u32 rh[16];
+  sha512_one_block(buf, 64, rh);
+  u32 r[8];
+  sc_reduce512(rh, r);
+  u32 R[8];
+  ge_p3_compress(base_scalarmult(r, sB), R);
+  _Pragma("unroll") for (int j = 0; j < 8; ++j) { buf[j] = R[j]; buf[8 + j] = pk[j]; buf[16 + j] = m[j]; }
+  u32 kh[16];
+  sha512_one_block(buf, 96, kh);
+  u32 k[8];
+  sc_reduce512(kh, k);
+  // s = (k * ar + r) mod l
+  u32 prod[16];
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) prod[j] = 0;
+  _Pragma("unroll") for (int x = 0; x < 8; ++x) {
+    u64 carry = 0;
+    _Pragma("unroll") for (int y = 0; y < 8; ++y) {
+      u64 t = (u64)k[x] * ar[y] + prod[x + y] + carry;
+      prod[x + y] = (u32)t;
+      carry = t >> 32;
+    }
+    prod[x + 8] = (u32)carry;
+  }
+  u64 carry = 0;
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) {
+    u64 t = (u64)prod[j] + (j < 8 ? r[j] : 0u) + carry;
+    prod[j] = (u32)t;
+    carry = t >> 32;
+  }
+  u32 s[8];
+  sc_reduce512(prod, s);
+  uint32_t* po = reinterpret_cast<uint32_t*>(pks + 32 * i);
+  uint32_t* so = reinterpret_cast<uint32_t*>(sigs + 64 * i);
+  _Pragma("unroll") for (int j = 0; j < 8; ++j) { po[j] = pk[j]; so[j] = R[j]; so[8 + j] = s[j]; }
+}
+
+// Seeds / messages of the synthetic workloads (SURVEY.md §8(d) cfg 2):
+//   out_i = SHA-512(tag || u64le(first + i))[..32]
+struct Tag64 { uint8_t b[64]; };
+__global__ void k_derive32(Tag64 tag, int taglen, uint64_t first, uint64_t n, uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  u32 words[28];
+  _Pragma("unroll") for (int j = 0; j < 28; ++j) words[j] = 0;
+  for (int b = 0; b < taglen; ++b) words[b >> 2] |= (u32)tag.b[b] << (8 * (b & 3));
+  const uint64_t v = first + i;
+  for (int b = 0; b < 8; ++b) {
+    const int pos = taglen + b;
+    words[pos >> 2] |= (u32)((v >> (8 * b)) & 0xFF) << (8 * (pos & 3));
+  }
+  u32 h[16];
+  sha512_one_block(words, taglen + 8, h);
+  uint32_t* o = reinterpret_cast<uint32_t*>(out + 32 * i);
+  _Pragma("unroll") for (int j = 0; j < 8; ++j) o[j] = h[j];
+}
+
+}  // namespace nwc

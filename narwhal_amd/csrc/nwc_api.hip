@@ -1,0 +1,469 @@
+// Host side of libnwc.so: the C ABI declared in include/nwc.h.
+//
+// One context per HIP device: its own stream, the basepoint table, and a growable staging
+// arena.  A per-device mutex makes every entry point thread-safe (the reference calls the
+// crypto crate from concurrent tokio tasks: primary/src/core.rs:88-114,
+// worker/src/worker.rs:182,227).  Host batch entry points shard independent units
+// (signatures, certificates, messages) over all initialised devices with one host thread per
+// device; nothing here ever falls back to a CPU path -- a device failure is
+// an error code (< 0), never a verdict.
+#include <hip/hip_runtime.h>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "nwc.h"
+#include "kernels.hip"
+
+namespace {
+
+thread_local std::string t_err;
+thread_local int t_dev = 0;
+
+int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  t_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return set_err(NWC_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),     \
+                     __FILE__, __LINE__);                                                       \
+  } while (0)
+
+struct DevCtx {
+  int hip_id = 0;
+  hipStream_t stream = nullptr;
+  nwc::ge_niels* base_table = nullptr;
+  uint8_t* arena = nullptr;
+  size_t arena_cap = 0;
+  std::mutex mu;
+
+  int ensure_arena(size_t bytes) {
+    if (bytes <= arena_cap) return 0;
+    if (arena) { (void)hipFree(arena); arena = nullptr; arena_cap = 0; }
+    size_t cap = bytes + bytes / 4 + (1 << 20);
+    HIP_TRY(hipMalloc(&arena, cap));
+    arena_cap = cap;
+    return 0;
+  }
+};
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<DevCtx>> g_devs;
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Carve {
+  uint8_t* base;
+  size_t off = 0;
+  explicit Carve(uint8_t* b) : base(b) {}
+  template <class T> T* take(size_t bytes) { T* p = reinterpret_cast<T*>(base + off); off += align256(bytes); return p; }
+};
+
+int init_device(DevCtx& d) {
+  HIP_TRY(hipSetDevice(d.hip_id));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, d.hip_id));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(NWC_ERR_NO_DEVICE, "device %d is %s; libnwc is built for gfx950 only", d.hip_id, prop.gcnArchName);
+  HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  HIP_TRY(hipMalloc(&d.base_table, 129 * sizeof(nwc::ge_niels)));
+  hipLaunchKernelGGL(nwc::k_build_base_table, dim3(3), dim3(64), 0, d.stream, d.base_table);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  return 0;
+}
+
+DevCtx* ctx(int i) {
+  if (i < 0 || i >= (int)g_devs.size()) return nullptr;
+  return g_devs[i].get();
+}
+
+int require_init() {
+  if (g_devs.empty()) return set_err(NWC_ERR_NOT_INIT, "nwc_init has not been called (or found no device)");
+  return 0;
+}
+
+// ---- launch helpers (caller holds the device mutex and has set the device) -----------------
+int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
+                  const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
+                  hipStream_t s) {
+  if (n == 0) return 0;
+  const uint64_t tiles = (n + 255) / 256;
+  const unsigned grid = (unsigned)(tiles < (1u << 20) ? tiles : (1u << 20));
+  hipLaunchKernelGGL(nwc::k_verify, dim3(grid), dim3(256), 0, s, msgs, msg_index, msg_stride, pks, sigs,
+                     out_words, n, strict, d.base_table);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int launch_digest(const uint8_t* data, const uint64_t* offsets, const uint64_t* ends, uint64_t n, uint8_t* out32,
+                  hipStream_t s) {
+  if (n == 0) return 0;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(nwc::k_sha512_digest32, dim3(grid), dim3(256), 0, s, data, offsets, ends, n, out32);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int launch_cert_reduce(const uint64_t* leaf, const uint32_t* offs, uint64_t m, uint64_t nvotes, uint64_t* cert,
+                       uint64_t* bad, hipStream_t s) {
+  const uint64_t words = (nvotes + 63) / 64;
+  const uint64_t threads = m > words ? m : words;
+  if (threads == 0) return 0;
+  const unsigned grid = (unsigned)((threads + 255) / 256);
+  hipLaunchKernelGGL(nwc::k_cert_reduce, dim3(grid), dim3(256), 0, s, leaf, offs, m, nvotes, cert, bad);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// Run fn(device_index, lo, hi) over [0, n) split across all devices, one host thread each.
+template <class F>
+int shard(uint64_t n, F fn) {
+  const int nd = (int)g_devs.size();
+  if (nd == 1 || n < 4096) return fn(0, (uint64_t)0, n);
+  std::vector<int> rc(nd, 0);
+  std::vector<std::thread> th;
+  const uint64_t per = (n + nd - 1) / nd;
+  for (int i = 0; i < nd; ++i) {
+    const uint64_t lo = std::min<uint64_t>(n, (uint64_t)i * per), hi = std::min<uint64_t>(n, lo + per);
+    th.emplace_back([&, i, lo, hi] {
+      rc[i] = fn(i, lo, hi);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int r : rc) if (r < 0) return r;
+  return 0;
+}
+
+// Copy `nbits` bits of device verdict words to a host bitmap starting at bit `bit0`.
+void merge_bits(uint8_t* dst, uint64_t bit0, const std::vector<uint64_t>& words, uint64_t nbits) {
+  if ((bit0 & 7) == 0) {
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(words.data());
+    const uint64_t full = nbits / 8;
+    std::memcpy(dst + bit0 / 8, src, full);
+    for (uint64_t b = full * 8; b < nbits; ++b) {
+      const uint64_t o = bit0 + b;
+      const bool v = (words[b >> 6] >> (b & 63)) & 1;
+      dst[o >> 3] = (uint8_t)((dst[o >> 3] & ~(1u << (o & 7))) | ((unsigned)v << (o & 7)));
+    }
+    return;
+  }
+  for (uint64_t b = 0; b < nbits; ++b) {
+    const uint64_t o = bit0 + b;
+    const bool v = (words[b >> 6] >> (b & 63)) & 1;
+    dst[o >> 3] = (uint8_t)((dst[o >> 3] & ~(1u << (o & 7))) | ((unsigned)v << (o & 7)));
+  }
+}
+
+// Host-memory verification of equations [lo, hi) on device di.
+int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_t* msg_index,
+                 const uint8_t* pks, const uint8_t* sigs, uint64_t lo, uint64_t hi, int strict,
+                 std::vector<uint64_t>& out_words, uint64_t nmsgs) {
+  DevCtx& d = *ctx(di);
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  const uint64_t n = hi - lo;
+  const uint64_t words = (n + 63) / 64;
+  out_words.assign(words, 0);
+  if (n == 0) return 0;
+  const uint64_t msg_bytes = msg_index ? 32 * nmsgs : (msg_stride ? 32 * n : 32);
+  const size_t need = align256(msg_bytes) + align256(msg_index ? 4 * n : 0) + align256(32 * n) + align256(64 * n) +
+                      align256(8 * words);
+  if (int rc = d.ensure_arena(need)) return rc;
+  Carve c(d.arena);
+  uint8_t* dm = c.take<uint8_t>(msg_bytes);
+  uint32_t* dmi = msg_index ? c.take<uint32_t>(4 * n) : nullptr;
+  uint8_t* dp = c.take<uint8_t>(32 * n);
+  uint8_t* ds = c.take<uint8_t>(64 * n);
+  uint64_t* dout = c.take<uint64_t>(8 * words);
+  if (msg_index) {
+    HIP_TRY(hipMemcpyAsync(dm, msgs, msg_bytes, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(dmi, msg_index + lo, 4 * n, hipMemcpyHostToDevice, d.stream));
+  } else {
+    HIP_TRY(hipMemcpyAsync(dm, msgs + (msg_stride ? 32 * lo : 0), msg_bytes, hipMemcpyHostToDevice, d.stream));
+  }
+  HIP_TRY(hipMemcpyAsync(dp, pks + 32 * lo, 32 * n, hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(hipMemcpyAsync(ds, sigs + 64 * lo, 64 * n, hipMemcpyHostToDevice, d.stream));
+  if (int rc = launch_verify(d, dm, dmi, msg_stride ? 1 : 0, dp, ds, n, strict, dout, d.stream)) return rc;
+  HIP_TRY(hipMemcpyAsync(out_words.data(), dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nwc_version(void) { return (1 << 16) | 0; }
+
+const char* nwc_last_error(void) { return t_err.c_str(); }
+
+int nwc_init(uint32_t device_mask) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_devs.empty()) return 0;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0)
+    return set_err(NWC_ERR_NO_DEVICE, "no HIP device visible (%s)", hipGetErrorString(e));
+  if (device_mask == 0) device_mask = 1;
+  for (int i = 0; i < count && i < 32; ++i) {
+    if (!((device_mask >> i) & 1)) continue;
+    auto d = std::make_unique<DevCtx>();
+    d->hip_id = i;
+    if (int rc = init_device(*d)) { g_devs.clear(); return rc; }
+    g_devs.push_back(std::move(d));
+  }
+  if (g_devs.empty()) return set_err(NWC_ERR_NO_DEVICE, "device mask 0x%x selects no visible device", device_mask);
+  return 0;
+}
+
+void nwc_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& d : g_devs) {
+    std::lock_guard<std::mutex> dl(d->mu);
+    (void)hipSetDevice(d->hip_id);
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
+    if (d->arena) (void)hipFree(d->arena);
+    if (d->base_table) (void)hipFree(d->base_table);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+  }
+  g_devs.clear();
+}
+
+int nwc_device_count(void) { return (int)g_devs.size(); }
+
+int nwc_verify_strict_many(const uint8_t* msgs32, const uint8_t* pks, const uint8_t* sigs, size_t n,
+                           uint8_t* verdict_bitmap) {
+  if (int rc = require_init()) return rc;
+  if (n && (!msgs32 || !pks || !sigs || !verdict_bitmap)) return set_err(NWC_ERR_ARG, "null buffer");
+  return shard(n, [&](int di, uint64_t lo, uint64_t hi) -> int {
+    std::vector<uint64_t> words;
+    int rc = verify_range(di, msgs32, 1, nullptr, pks, sigs, lo, hi, 1, words, 0);
+    if (rc) return rc;
+    merge_bits(verdict_bitmap, lo, words, hi - lo);
+    return 0;
+  });
+}
+
+int nwc_verify_strict(const uint8_t msg32[32], const uint8_t pk[32], const uint8_t sig[64]) {
+  uint8_t bit = 0;
+  int rc = nwc_verify_strict_many(msg32, pk, sig, 1, &bit);
+  if (rc < 0) return rc;
+  return (bit & 1) ? NWC_OK : NWC_INVALID;
+}
+
+int nwc_verify_batch(const uint8_t msg32[32], const uint8_t* pks, const uint8_t* sigs, size_t n,
+                     uint8_t* bad_bitmap) {
+  if (int rc = require_init()) return rc;
+  if (n == 0) return NWC_OK;  // empty iterator: dalek verify_batch of nothing is Ok
+  if (!msg32 || !pks || !sigs) return set_err(NWC_ERR_ARG, "null buffer");
+  std::vector<uint64_t> words;
+  if (int rc = verify_range(t_dev < (int)g_devs.size() ? t_dev : 0, msg32, 0, nullptr, pks, sigs, 0, n, 0, words, 0))
+    return rc;
+  bool all = true;
+  for (size_t i = 0; i < n; ++i) all = all && ((words[i >> 6] >> (i & 63)) & 1);
+  if (bad_bitmap) {
+    std::vector<uint64_t> bad(words.size());
+    for (size_t w = 0; w < words.size(); ++w) bad[w] = ~words[w];
+    merge_bits(bad_bitmap, 0, bad, n);
+  }
+  return all ? NWC_OK : NWC_INVALID;
+}
+
+int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks, const uint8_t* sigs,
+                          size_t m, uint8_t* cert_ok_bitmap, uint8_t* bad_vote_bitmap) {
+  if (int rc = require_init()) return rc;
+  if (m == 0) return 0;
+  if (!digests || !offsets || !cert_ok_bitmap) return set_err(NWC_ERR_ARG, "null buffer");
+  if (offsets[0] != 0) return set_err(NWC_ERR_ARG, "offsets[0] must be 0");
+  for (size_t c = 0; c < m; ++c)
+    if (offsets[c + 1] < offsets[c]) return set_err(NWC_ERR_ARG, "offsets not monotone at %zu", c);
+  const uint64_t nv = offsets[m];
+  if (nv && (!pks || !sigs)) return set_err(NWC_ERR_ARG, "null vote buffer");
+  // vote -> certificate index (host side; the kernel reads digests through it)
+  std::vector<uint32_t> mi(nv);
+  for (size_t c = 0; c < m; ++c)
+    for (uint32_t v = offsets[c]; v < offsets[c + 1]; ++v) mi[v] = (uint32_t)c;
+  std::vector<uint64_t> leaf((nv + 63) / 64, 0);
+  // shard votes on certificate boundaries
+  const int nd = (int)g_devs.size();
+  std::vector<uint64_t> cuts{0};
+  for (int i = 1; i < nd; ++i) {
+    uint64_t target = nv * i / nd;
+    size_t c = 0;
+    while (c < m && offsets[c] < target) ++c;
+    cuts.push_back(offsets[c]);
+  }
+  cuts.push_back(nv);
+  std::vector<int> rc(nd, 0);
+  std::vector<std::vector<uint64_t>> parts(nd);
+  std::vector<std::thread> th;
+  for (int i = 0; i < nd; ++i) {
+    th.emplace_back([&, i] {
+      rc[i] = verify_range(i, digests, 0, mi.data(), pks, sigs, cuts[i], cuts[i + 1], 0, parts[i], m);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int r : rc) if (r < 0) return r;
+  std::vector<uint8_t> leafbytes((nv + 7) / 8 + 8, 0);
+  for (int i = 0; i < nd; ++i) merge_bits(leafbytes.data(), cuts[i], parts[i], cuts[i + 1] - cuts[i]);
+  std::memset(cert_ok_bitmap, 0, (m + 7) / 8);
+  for (size_t c = 0; c < m; ++c) {
+    bool ok = true;
+    for (uint32_t v = offsets[c]; v < offsets[c + 1]; ++v) ok = ok && ((leafbytes[v >> 3] >> (v & 7)) & 1);
+    if (ok) cert_ok_bitmap[c >> 3] |= (uint8_t)(1u << (c & 7));
+  }
+  if (bad_vote_bitmap) {
+    for (uint64_t v = 0; v < nv; ++v) {
+      const bool bad = !((leafbytes[v >> 3] >> (v & 7)) & 1);
+      bad_vote_bitmap[v >> 3] = (uint8_t)((bad_vote_bitmap[v >> 3] & ~(1u << (v & 7))) | ((unsigned)bad << (v & 7)));
+    }
+  }
+  return 0;
+}
+
+int nwc_set_committee(const uint8_t* pks, size_t n) {
+  if (int rc = require_init()) return rc;
+  if (n && !pks) return set_err(NWC_ERR_ARG, "null buffer");
+  return 0;  // verdicts never depend on the cache; keys are decoded per equation in this version
+}
+
+int nwc_sha512_trunc32_many(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32) {
+  if (int rc = require_init()) return rc;
+  if (n == 0) return 0;
+  if (!offsets || !out32) return set_err(NWC_ERR_ARG, "null buffer");
+  for (size_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return set_err(NWC_ERR_ARG, "offsets not monotone at %zu", i);
+  if (offsets[n] > offsets[0] && !data) return set_err(NWC_ERR_ARG, "null data");
+  return shard(n, [&](int di, uint64_t lo, uint64_t hi) -> int {
+    DevCtx& d = *ctx(di);
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.hip_id));
+    const uint64_t k = hi - lo;
+    if (k == 0) return 0;
+    // Device layout: every message starts 16-byte aligned (the kernel's dwordx4 path).
+    std::vector<uint64_t> starts(k), ends(k);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < k; ++i) {
+      const uint64_t len = offsets[lo + i + 1] - offsets[lo + i];
+      starts[i] = total;
+      ends[i] = total + len;
+      total += (len + 15) & ~15ull;
+    }
+    const size_t need = align256(total + 16) + 2 * align256(8 * k) + align256(32 * k);
+    if (int rc = d.ensure_arena(need)) return rc;
+    Carve c(d.arena);
+    uint8_t* dd = c.take<uint8_t>(total + 16);
+    uint64_t* dstarts = c.take<uint64_t>(8 * k);
+    uint64_t* dends = c.take<uint64_t>(8 * k);
+    uint8_t* dout = c.take<uint8_t>(32 * k);
+    const bool aligned = (offsets[lo] % 16 == 0) && [&] {
+      for (uint64_t i = 0; i < k; ++i) if (offsets[lo + i] - offsets[lo] != starts[i]) return false;
+      return true;
+    }();
+    if (aligned) {
+      if (total) HIP_TRY(hipMemcpyAsync(dd, data + offsets[lo], offsets[hi] - offsets[lo], hipMemcpyHostToDevice, d.stream));
+    } else {
+      std::vector<uint8_t> stage(total);
+      for (uint64_t i = 0; i < k; ++i)
+        if (ends[i] > starts[i]) std::memcpy(stage.data() + starts[i], data + offsets[lo + i], ends[i] - starts[i]);
+      if (total) HIP_TRY(hipMemcpyAsync(dd, stage.data(), total, hipMemcpyHostToDevice, d.stream));
+      HIP_TRY(hipStreamSynchronize(d.stream));  // `stage` is pageable and about to go out of scope
+    }
+    HIP_TRY(hipMemcpyAsync(dstarts, starts.data(), 8 * k, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(dends, ends.data(), 8 * k, hipMemcpyHostToDevice, d.stream));
+    if (int rc = launch_digest(dd, dstarts, dends, k, dout, d.stream)) return rc;
+    HIP_TRY(hipMemcpyAsync(out32 + 32 * lo, dout, 32 * k, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    return 0;
+  });
+}
+
+int nwc_digest32(const uint8_t* data, size_t len, uint8_t out32[32]) {
+  uint64_t offs[2] = {0, (uint64_t)len};
+  return nwc_sha512_trunc32_many(data, offs, 1, out32);
+}
+
+// ---- device-resident ---------------------------------------------------------------------
+int nwc_dev_set_device(int device) {
+  if (int rc = require_init()) return rc;
+  if (device < 0 || device >= (int)g_devs.size()) return set_err(NWC_ERR_ARG, "device %d not initialised", device);
+  t_dev = device;
+  return 0;
+}
+
+#define DEV_PROLOGUE                                                        \
+  if (int rc_ = require_init()) return rc_;                                 \
+  DevCtx& d = *ctx(t_dev < (int)g_devs.size() ? t_dev : 0);                 \
+  std::lock_guard<std::mutex> lk(d.mu);                                     \
+  HIP_TRY(hipSetDevice(d.hip_id));                                          \
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream); /* NULL = HIP default stream */
+
+int nwc_dev_verify(const void* d_msgs, const void* d_msg_index, uint64_t msg_stride, const void* d_pks,
+                   const void* d_sigs, uint64_t n, int strict, void* d_verdict_words, void* stream) {
+  DEV_PROLOGUE
+  if (n && (!d_msgs || !d_pks || !d_sigs || !d_verdict_words)) return set_err(NWC_ERR_ARG, "null buffer");
+  return launch_verify(d, (const uint8_t*)d_msgs, (const uint32_t*)d_msg_index, msg_stride, (const uint8_t*)d_pks,
+                       (const uint8_t*)d_sigs, n, strict, (uint64_t*)d_verdict_words, s);
+}
+
+int nwc_dev_cert_reduce(const void* d_leaf_words, const void* d_offsets, uint64_t m, uint64_t nvotes,
+                        void* d_cert_words, void* d_bad_words, void* stream) {
+  DEV_PROLOGUE
+  return launch_cert_reduce((const uint64_t*)d_leaf_words, (const uint32_t*)d_offsets, m, nvotes,
+                            (uint64_t*)d_cert_words, (uint64_t*)d_bad_words, s);
+}
+
+int nwc_dev_sha512_trunc32(const void* d_data, const void* d_offsets, uint64_t n, void* d_out32, void* stream) {
+  DEV_PROLOGUE
+  return launch_digest((const uint8_t*)d_data, (const uint64_t*)d_offsets, nullptr, n, (uint8_t*)d_out32, s);
+}
+
+int nwc_dev_sha512_trunc32_ranges(const void* d_data, const void* d_starts, const void* d_ends, uint64_t n,
+                                  void* d_out32, void* stream) {
+  DEV_PROLOGUE
+  if (n && (!d_starts || !d_ends || !d_out32)) return set_err(NWC_ERR_ARG, "null buffer");
+  return launch_digest((const uint8_t*)d_data, (const uint64_t*)d_starts, (const uint64_t*)d_ends, n,
+                       (uint8_t*)d_out32, s);
+}
+
+int nwc_dev_derive32(const uint8_t* tag, int taglen, uint64_t first, uint64_t n, void* d_out, void* stream) {
+  DEV_PROLOGUE
+  if (taglen < 0 || taglen > 96) return set_err(NWC_ERR_ARG, "tag longer than 96 bytes");
+  if (n == 0) return 0;
+  nwc::Tag64 t;
+  std::memset(&t, 0, sizeof t);
+  if (taglen > 64) return set_err(NWC_ERR_ARG, "tag longer than 64 bytes");
+  std::memcpy(t.b, tag, (size_t)taglen);
+  hipLaunchKernelGGL(nwc::k_derive32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, t, taglen, first, n,
+                     (uint8_t*)d_out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int nwc_dev_keygen_sign(const void* d_seeds, const void* d_msgs, uint64_t n, void* d_pks, void* d_sigs,
+                        void* stream) {
+  DEV_PROLOGUE
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(nwc::k_keygen_sign, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const uint8_t*)d_seeds,
+                     (const uint8_t*)d_msgs, n, (uint8_t*)d_pks, (uint8_t*)d_sigs, d.base_table);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"
