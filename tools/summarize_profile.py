@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Condenses a round's rocprofv3 output (tools/profile_round.sh) into profiles/<tag>/:
+kernel_stats.csv (as produced), pmc_*.csv filtered to the nwc:: kernels, and summary.json with
+per-kernel average duration, VALU instructions per lane, VALU lane-op rate, FETCH_SIZE bytes.
+
+    python tools/summarize_profile.py gpurun_out/prof_r01 profiles/r01
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+VALU_PEAK = 64 * 256 * 2.4e9  # VOP3 lane-ops/s
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
+    summary = {}
+    for name, r in stats.items():
+        if not name.startswith("nwc::"):
+            continue
+        summary[name.split("(")[0]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                       "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
+    for pmc in ("pmc_sq", "pmc_fetch"):
+        path = os.path.join(src, pmc, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        rows = [r for r in csv.DictReader(open(path)) if r["Kernel_Name"].startswith("nwc::")]
+        with open(os.path.join(dst, pmc + ".csv"), "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+            w.writeheader()
+            w.writerows(rows)
+        agg = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in rows:
+            agg[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, cs in agg.items():
+            d = summary.setdefault(k, {})
+            for c, v in cs.items():
+                d[c] = sum(v) / len(v)
+            d["VGPR"] = int(rows[[r["Kernel_Name"].split("(")[0] for r in rows].index(k)]["VGPR_Count"])
+            d["AGPR"] = int(rows[[r["Kernel_Name"].split("(")[0] for r in rows].index(k)]["Accum_VGPR_Count"])
+            d["scratch_per_lane"] = int(rows[[r["Kernel_Name"].split("(")[0] for r in rows].index(k)]["Scratch_Size"])
+    for k, d in summary.items():
+        if "SQ_INSTS_VALU" in d and "avg_ns" in d and d.get("SQ_WAVES"):
+            d["valu_insts_per_lane"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
+            d["valu_lane_ops_per_s"] = d["SQ_INSTS_VALU"] * 64 / (d["avg_ns"] * 1e-9)
+            d["valu_issue_frac"] = d["valu_lane_ops_per_s"] / VALU_PEAK
+        if "FETCH_SIZE" in d:
+            d["fetch_bytes_reported"] = d["FETCH_SIZE"] * 1024
+            d["fetch_bytes_x2_gfx950"] = d["FETCH_SIZE"] * 1024 * 2
+    json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
