@@ -103,14 +103,61 @@ __global__ void k_build_base_table(ge_niels* table) {
 }
 
 // ------------------------------------------------------------------------------- ladder
-// R' = k*P + s*B where P is given by its 9-entry cached table tab[0..8] = {O, P, 2P, .., 8P}.
-// kd: radix-16 digits of k (nibble d+8), sd: radix-256 digits of s (byte d+128).
-__device__ __noinline__ ge_p2 double_scalarmult(const ge_cached* tab, u32 kd[8], u32 sd[8],
-                                                const ge_niels* sB) {
+// Per-lane table of the variable base in global scratch, lane-contiguous: 9 entries x 160 B
+// (cached point = 40 dwords = 10 x dwordx4).  A lookup reads one lane's 160 contiguous bytes,
+// so a wave touches ~128 lines per lookup instead of the whole wave's table (the compiler's
+// private memory interleaves lanes dword by dword).
+constexpr int TAB_ENTRIES = 9;
+constexpr int TAB_U4_PER_ENTRY = 10;
+constexpr size_t TAB_BYTES_PER_LANE = TAB_ENTRIES * TAB_U4_PER_ENTRY * 16;   // 1440
+
+struct LaneTable {
+  uint4* p;
+  __device__ __forceinline__ void store(int e, const ge_cached& c) const {
+    const uint4* src = reinterpret_cast<const uint4*>(&c);
+    _Pragma("unroll") for (int i = 0; i < TAB_U4_PER_ENTRY; ++i) p[e * TAB_U4_PER_ENTRY + i] = src[i];
+  }
+  __device__ __forceinline__ ge_cached load(int e) const {
+    ge_cached c;
+    uint4* dst = reinterpret_cast<uint4*>(&c);
+    _Pragma("unroll") for (int i = 0; i < TAB_U4_PER_ENTRY; ++i) dst[i] = p[e * TAB_U4_PER_ENTRY + i];
+    return c;
+  }
+};
+static_assert(sizeof(ge_cached) == TAB_U4_PER_ENTRY * 16, "cached point layout");
+
+// tab[j] = j * P for j = 0..8 (tab[0] = identity)
+__device__ __forceinline__ void build_table(const LaneTable& tab, const ge_p3& P) {
+  ge_cached p1 = ge_p3_to_cached(P);
+  tab.store(0, ge_cached_identity());
+  tab.store(1, p1);
+  ge_p3 pj = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
+  tab.store(2, ge_p3_to_cached(pj));
+#pragma unroll 1
+  for (int j = 3; j < TAB_ENTRIES; ++j) {
+    pj = ge_p1p1_to_p3(ge_add_cached(pj, p1));
+    tab.store(j, ge_p3_to_cached(pj));
+  }
+}
+
+// R' = k*P + s*B with P's table in `tab`, kd: radix-16 digits of k (nibble d+8), sd: radix-256
+// digits of s (byte d+128), sB: basepoint table in LDS.  Uniform schedule: every lane adds at
+// every window.  The next window's table entry is loaded while this window's doublings run.
+__device__ __forceinline__ ge_p2 double_scalarmult(const LaneTable& tab, u32 kd[8], u32 sd[8],
+                                                   const ge_niels* sB) {
   ge_p3 acc = ge_p3_identity();
   ge_p1p1 t;
+  i32 dk = (i32)(kd[7] >> 28) - 8;
+  digits_shl(kd, 4);
+  ge_cached nxt = tab.load(dk < 0 ? -dk : dk);
 #pragma unroll 1
   for (int w = 63; w >= 0; --w) {
+    const ge_cached cur = ge_cached_cneg(nxt, dk < 0);
+    if (w > 0) {
+      dk = (i32)(kd[7] >> 28) - 8;
+      digits_shl(kd, 4);
+      nxt = tab.load(dk < 0 ? -dk : dk);
+    }
     if (w != 63) {
       ge_p2 p2 = ge_p1p1_to_p2(t);
       t = ge_p2_dbl(p2);
@@ -122,17 +169,11 @@ __device__ __noinline__ ge_p2 double_scalarmult(const ge_cached* tab, u32 kd[8],
       t = ge_p2_dbl(p2);
       acc = ge_p1p1_to_p3(t);
     }
-    // k digit: top nibble of kd
-    const i32 dk = (i32)(kd[7] >> 28) - 8;
-    digits_shl(kd, 4);
-    const int ak = dk < 0 ? -dk : dk;
-    ge_cached e = tab[ak];
-    t = ge_add_cached(acc, ge_cached_cneg(e, dk < 0));
+    t = ge_add_cached(acc, cur);
     if ((w & 1) == 0) {
       const i32 ds = (i32)(sd[7] >> 24) - 128;
       digits_shl(sd, 8);
-      const int as = ds < 0 ? -ds : ds;
-      ge_niels nb = sB[as];
+      const ge_niels nb = sB[ds < 0 ? -ds : ds];
       acc = ge_p1p1_to_p3(t);
       t = ge_add_niels(acc, ge_niels_cneg(nb, ds < 0));
     }
@@ -144,9 +185,10 @@ __device__ __noinline__ bool decompress_point(ge_p3& out, const u32 w[8], u32 yc
   return ge_decompress(out, w, ycanon);
 }
 
-// One verification equation.  Returns the verdict bit.
+// One verification equation (strict: dalek verify_strict; else the batch leaf).  Returns the
+// verdict bit.  `tab` is this lane's table slot.
 __device__ bool verify_one(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict,
-                           const ge_niels* sB) {
+                           const ge_niels* sB, const LaneTable& tab) {
   u32 rw[8], sw[8];
   _Pragma("unroll") for (int i = 0; i < 8; ++i) { rw[i] = sigw[i]; sw[i] = sigw[8 + i]; }
   const bool s_ok = sc_lt_l(sw);
@@ -154,6 +196,7 @@ __device__ bool verify_one(const u32 mw[8], const u32 aw[8], const u32 sigw[16],
   ge_p3 A, R;
   u32 ya[8], yr[8];
   const bool a_ok = decompress_point(A, aw, ya);
+  build_table(tab, ge_p3_neg(A));          // table of -A multiples
   const bool r_ok = decompress_point(R, rw, yr);
   const bool small = strict && (ycanon_is_small_order(ya) || ycanon_is_small_order(yr));
 
@@ -175,23 +218,10 @@ __device__ bool verify_one(const u32 mw[8], const u32 aw[8], const u32 sigw[16],
   }
   u32 kw[8];
   sc_reduce512(hw, kw);
-
-  // table of -A multiples: tab[j] = j * (-A)
-  ge_cached tab[9];
-  ge_p3 na = ge_p3_neg(A);
-  tab[0] = ge_cached_identity();
-  tab[1] = ge_p3_to_cached(na);
-  ge_p3 pj = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(na)));
-  tab[2] = ge_p3_to_cached(pj);
-#pragma unroll 1
-  for (int j = 3; j <= 8; ++j) {
-    pj = ge_p1p1_to_p3(ge_add_cached(pj, tab[1]));
-    tab[j] = ge_p3_to_cached(pj);
-  }
   u32 kd[8], sd[8];
   sc_recode_radix16(kw, kd);
   sc_recode_radix256(sw, sd);
-  ge_p2 rp = double_scalarmult(tab, kd, sd, sB);
+  const ge_p2 rp = double_scalarmult(tab, kd, sd, sB);
 
   // R' == R  <=>  X' == x_R Z'  and  Y' == y_R Z'   (R affine: Z = 1)
   const bool eq = fe_is_zero(fe_sub(rp.X, fe_mul(R.X, rp.Z))) && fe_is_zero(fe_sub(rp.Y, fe_mul(R.Y, rp.Z)));
@@ -201,17 +231,21 @@ __device__ bool verify_one(const u32 mw[8], const u32 aw[8], const u32 sigw[16],
 // ------------------------------------------------------------------------------- verify
 // n equations; equation i uses msgs[32 * (msg_index ? msg_index[i] : i * msg_stride)], pks[32 i],
 // sigs[64 i] (msg_stride 0 broadcasts one digest: Signature::verify_batch, crypto/src/lib.rs:214).
-// out_bits[i / 64] bit (i % 64) = verdict.  Grid-stride over 256-lane tiles.
+// out_bits[i / 64] bit (i % 64) = verdict.  Persistent grid: block b processes 256-lane tiles
+// b, b + gridDim.x, ...; lane slot (blockIdx.x * 256 + threadIdx.x) of `scratch` holds its table.
 __global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ msgs,
                                                 const uint32_t* __restrict__ msg_index, uint64_t msg_stride,
                                                 const uint8_t* __restrict__ pks,
                                                 const uint8_t* __restrict__ sigs,
                                                 uint64_t* __restrict__ out_bits, uint64_t n,
-                                                int strict, const ge_niels* __restrict__ base_table) {
+                                                int strict, const ge_niels* __restrict__ base_table,
+                                                uint8_t* __restrict__ scratch) {
   __shared__ ge_niels sB[129];
   for (int i = threadIdx.x; i < 129 * 30; i += blockDim.x)
     reinterpret_cast<i32*>(sB)[i] = reinterpret_cast<const i32*>(base_table)[i];
   __syncthreads();
+  const LaneTable tab{reinterpret_cast<uint4*>(scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) *
+                                                             TAB_BYTES_PER_LANE)};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
     const uint64_t i = base + threadIdx.x;
@@ -223,7 +257,7 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ msgs
     load_words8(pks + 32 * ii, aw);
     load_words8(sigs + 64 * ii, sgw);
     load_words8(sigs + 64 * ii + 32, sgw + 8);
-    bool v = verify_one(mw, aw, sgw, strict != 0, sB) && active;
+    bool v = verify_one(mw, aw, sgw, strict != 0, sB, tab) && active;
     const uint64_t ballot = __ballot(v);
     if ((threadIdx.x & 63) == 0 && base + (threadIdx.x & ~63u) < n) out_bits[(base + threadIdx.x) >> 6] = ballot;
   }

@@ -46,8 +46,15 @@ int set_err(int code, const char* fmt, ...) {
 
 struct DevCtx {
   int hip_id = 0;
+  int cus = 0;
+  int verify_blocks_per_cu = 1;
   hipStream_t stream = nullptr;
   nwc::ge_niels* base_table = nullptr;
+  // k_verify per-lane table slots; reused by every launch, so launches that use it are
+  // serialised across streams with `scratch_free` (recorded after each such launch).
+  uint8_t* scratch = nullptr;
+  size_t scratch_cap = 0;
+  hipEvent_t scratch_free = nullptr;
   uint8_t* arena = nullptr;
   size_t arena_cap = 0;
   std::mutex mu;
@@ -81,6 +88,11 @@ int init_device(DevCtx& d) {
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return set_err(NWC_ERR_NO_DEVICE, "device %d is %s; libnwc is built for gfx950 only", d.hip_id, prop.gcnArchName);
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&d.scratch_free, hipEventDisableTiming));
+  d.cus = prop.multiProcessorCount;
+  int bpc = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify), 256, 0));
+  d.verify_blocks_per_cu = bpc > 0 ? bpc : 1;
   HIP_TRY(hipMalloc(&d.base_table, 129 * sizeof(nwc::ge_niels)));
   hipLaunchKernelGGL(nwc::k_build_base_table, dim3(3), dim3(64), 0, d.stream, d.base_table);
   HIP_TRY(hipGetLastError());
@@ -104,10 +116,24 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
                   hipStream_t s) {
   if (n == 0) return 0;
   const uint64_t tiles = (n + 255) / 256;
-  const unsigned grid = (unsigned)(tiles < (1u << 20) ? tiles : (1u << 20));
+  // persistent grid: a few blocks per resident slot so the tail is short
+  const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * 4;
+  const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
+  const size_t need = (size_t)grid * 256 * nwc::TAB_BYTES_PER_LANE;
+  if (need > d.scratch_cap) {
+    HIP_TRY(hipEventSynchronize(d.scratch_free));
+    if (d.scratch) HIP_TRY(hipFree(d.scratch));
+    d.scratch = nullptr;
+    d.scratch_cap = 0;
+    const size_t full = (size_t)cap * 256 * nwc::TAB_BYTES_PER_LANE;
+    HIP_TRY(hipMalloc(&d.scratch, full));
+    d.scratch_cap = full;
+  }
+  HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
   hipLaunchKernelGGL(nwc::k_verify, dim3(grid), dim3(256), 0, s, msgs, msg_index, msg_stride, pks, sigs,
-                     out_words, n, strict, d.base_table);
+                     out_words, n, strict, d.base_table, d.scratch);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(d.scratch_free, s));
   return 0;
 }
 
@@ -239,6 +265,8 @@ void nwc_shutdown(void) {
     (void)hipSetDevice(d->hip_id);
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     if (d->arena) (void)hipFree(d->arena);
+    if (d->scratch) (void)hipFree(d->scratch);
+    if (d->scratch_free) (void)hipEventDestroy(d->scratch_free);
     if (d->base_table) (void)hipFree(d->base_table);
     if (d->stream) (void)hipStreamDestroy(d->stream);
   }
