@@ -42,7 +42,9 @@ METRIC = "Ed25519 verifies/sec at 1/2/4/8 MI355X (+% int-VALU peak); batch diges
 # projective compare) + one SHA-512 block.  Converted to 32-bit-lane VALU instructions with the
 # per-op instruction counts of this build's fe_sq / fe_mul / sha512_compress (tools/count_ops.py).
 W_S, W_M, W_SHA = 1546, 1429, 1
-OPS_S, OPS_M, OPS_SHA = None, None, None  # filled from tools/op_counts.json
+# Frozen at the round-1 build (tools/count_ops.py on commit dc19643, before any kernel tuning):
+# later speedups of fe_mul/fe_sq must raise `frac`, not shrink the work they are measured against.
+OPS_S, OPS_M, OPS_SHA = 134, 167, 5039
 # int-VALU issue peak: 64 lane-instructions / clk / CU for VOP3-class ops (v_mad_u64_u32,
 # v_mad_i64_i32, v_alignbit, v_bitop3 ...; tools/microbench/int_rates.hip) x 256 CU x 2.4 GHz
 VALU_PEAK_TOPS = 64 * 256 * 2.4e9 / 1e12      # 39.32 T lane-ops/s
@@ -51,13 +53,6 @@ HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md (spec)
 CFG4_TXS, CFG4_TX_BYTES = 977, 512
 CFG4_BATCH_BYTES = 12 + CFG4_TXS * (8 + CFG4_TX_BYTES)   # 508,052
 CFG4_STRIDE = (CFG4_BATCH_BYTES + 255) & ~255
-
-
-def load_op_counts():
-    global OPS_S, OPS_M, OPS_SHA
-    with open(os.path.join(ROOT, "tools", "op_counts.json")) as f:
-        c = json.load(f)
-    OPS_S, OPS_M, OPS_SHA = c["fe_sq"], c["fe_mul"], c["sha512_block"]
 
 
 def ops_per_verify() -> float:
@@ -224,7 +219,6 @@ def main():
     rank, world, local = dist_setup(args)
     from narwhal_amd import _lib, device
     _lib.load(device_mask=1 << local)   # the library drives the same GPU as this rank
-    load_op_counts()
 
     # ---------------- verify leg (headline)
     n = args.n

@@ -48,21 +48,32 @@ FE_DEV fe fe_select(const fe& a, const fe& b, bool c) {
   fe r; _Pragma("unroll") for (int i = 0; i < 10; ++i) r.v[i] = c ? b.v[i] : a.v[i]; return r;
 }
 
-// Carry-propagate 64-bit column sums into tight limbs.  Two interleaved chains
-// (0->1->2->3->4->5, 4->5->6->7->8->9->0) halve the dependent depth.
+// Column k's accumulator starts at the rounding bias 2^(w_k - 1) (w_k = 26 even, 25 odd), so
+// every carry is a floor shift (c = h >> w) and the remainder a mask; the bias is removed once
+// at the end, leaving centered limbs in [-2^(w-1), 2^(w-1)] (+ a small incoming carry on limbs
+// 1 and 5).  Two interleaved chains (0->1->2->3->4->5, 4->5->6->7->8->9->0) halve the depth.
+FE_DEV i64 fe_col_bias(int k) { return (k & 1) ? ((i64)1 << 24) : ((i64)1 << 25); }
+
 FE_DEV fe fe_carry_wide(i64 h[10]) {
   i64 c;
-#define FE_CARRY(i, sh) { c = (h[i] + ((i64)1 << (sh - 1))) >> sh; h[(i) + 1] += c; h[i] -= c << sh; }
-  FE_CARRY(0, 26); FE_CARRY(4, 26);
-  FE_CARRY(1, 25); FE_CARRY(5, 25);
-  FE_CARRY(2, 26); FE_CARRY(6, 26);
-  FE_CARRY(3, 25); FE_CARRY(7, 25);
-  FE_CARRY(4, 26); FE_CARRY(8, 26);
-  c = (h[9] + ((i64)1 << 24)) >> 25; h[0] += c * 19; h[9] -= c << 25;
-  FE_CARRY(0, 26);
-#undef FE_CARRY
-  fe r; _Pragma("unroll") for (int i = 0; i < 10; ++i) r.v[i] = (i32)h[i];
-  return r;
+  u32 r[10];
+#define FE_FLOOR(i, sh) { c = h[i] >> sh; r[i] = (u32)h[i] & ((1u << sh) - 1u); }
+  FE_FLOOR(0, 26); h[1] += c;
+  FE_FLOOR(4, 26); h[5] += c;
+  FE_FLOOR(1, 25); h[2] += c;
+  FE_FLOOR(5, 25); h[6] += c;
+  FE_FLOOR(2, 26); h[3] += c;
+  FE_FLOOR(6, 26); h[7] += c;
+  FE_FLOOR(3, 25); h[4] = (i64)r[4] + c;
+  FE_FLOOR(7, 25); h[8] += c;
+  FE_FLOOR(4, 26); r[5] += (u32)c;           // c < 2^12 here
+  FE_FLOOR(8, 26); h[9] += c;
+  FE_FLOOR(9, 25); h[0] = (i64)r[0] + c * 19;
+  FE_FLOOR(0, 26); r[1] += (u32)c;           // c < 2^17 here
+#undef FE_FLOOR
+  fe out;
+  _Pragma("unroll") for (int i = 0; i < 10; ++i) out.v[i] = (i32)(r[i] - (u32)fe_col_bias(i));
+  return out;
 }
 
 // h = f * g.  Column k collects f_i g_j for i + j = k (mod 10); a wrapped term (i + j >= 10)
@@ -73,7 +84,7 @@ FE_DEV fe fe_mul(const fe& f, const fe& g) {
   _Pragma("unroll") for (int i = 0; i < 10; ++i) { g19[i] = (i32)(19u * (u32)g.v[i]); f2[i] = (i32)(2u * (u32)f.v[i]); }
   i64 h[10];
   _Pragma("unroll") for (int k = 0; k < 10; ++k) {
-    i64 acc = 0;
+    i64 acc = fe_col_bias(k);
     _Pragma("unroll") for (int i = 0; i < 10; ++i) {
       const int j = (k - i + 10) % 10;
       const bool wrap = (i + j) >= 10;
@@ -94,7 +105,7 @@ FE_DEV void fe_sq_wide(const fe& f, i64 h[10]) {
     f2[i] = (i32)(2u * (u32)f.v[i]); f19[i] = (i32)(19u * (u32)f.v[i]); f38[i] = (i32)(38u * (u32)f.v[i]);
   }
   _Pragma("unroll") for (int k = 0; k < 10; ++k) {
-    i64 acc = 0;
+    i64 acc = 0;   // fe_sq / fe_sq2 add the column bias after (fe_sq2 doubles first)
     _Pragma("unroll") for (int i = 0; i < 10; ++i) {
       _Pragma("unroll") for (int j = i; j < 10; ++j) {
         if ((i + j) % 10 != k) continue;
@@ -110,13 +121,17 @@ FE_DEV void fe_sq_wide(const fe& f, i64 h[10]) {
     h[k] = acc;
   }
 }
-FE_DEV fe fe_sq(const fe& f) { i64 h[10]; fe_sq_wide(f, h); return fe_carry_wide(h); }
+FE_DEV fe fe_sq(const fe& f) {
+  i64 h[10]; fe_sq_wide(f, h);
+  _Pragma("unroll") for (int i = 0; i < 10; ++i) h[i] += fe_col_bias(i);
+  return fe_carry_wide(h);
+}
 
 // 2 f^2, doubled before the carry so the result is tight (the 2Z^2 term of point doubling
 // is then combined with two more tight terms and stays within the loose bound).
 FE_DEV fe fe_sq2(const fe& f) {
   i64 h[10]; fe_sq_wide(f, h);
-  _Pragma("unroll") for (int i = 0; i < 10; ++i) h[i] += h[i];
+  _Pragma("unroll") for (int i = 0; i < 10; ++i) h[i] = h[i] + h[i] + fe_col_bias(i);
   return fe_carry_wide(h);
 }
 
@@ -128,7 +143,7 @@ FE_DEV fe fe_sqn(fe f, int n) {
 // Multiply by a small constant (|c| < 2^5): used for d-free formulas only.
 FE_DEV fe fe_mul_small(const fe& f, i32 c) {
   i64 h[10];
-  _Pragma("unroll") for (int i = 0; i < 10; ++i) h[i] = (i64)f.v[i] * c;
+  _Pragma("unroll") for (int i = 0; i < 10; ++i) h[i] = (i64)f.v[i] * c + fe_col_bias(i);
   return fe_carry_wide(h);
 }
 

@@ -100,33 +100,76 @@ FE_DEV ge_niels ge_niels_cneg(const ge_niels& q, bool neg) {
   return r;
 }
 
-// curve25519-dalek CompressedEdwardsY::decompress:
+// curve25519-dalek CompressedEdwardsY::decompress of TWO encodings at once:
 //   y = low 255 bits (y >= p accepted), u = y^2 - 1, v = d y^2 + 1, (ok, x) = sqrt_ratio_i(u, v),
 //   x := -x if the sign bit is set -- even when x == 0.
-// Also returns the canonical y words (for the small-order test and the caller's use).
-FE_DEV bool ge_decompress(ge_p3& out, const u32 w[8], u32 ycanon[8]) {
-  fe y = fe_from_words(w);
-  fe one = fe_one();
-  fe yy = fe_sq(y);
-  fe u = fe_sub(yy, one);
-  fe v = fe_add(fe_mul(yy, FE_D), one);
-  fe v3 = fe_mul(fe_sq(v), v);
-  fe v7 = fe_mul(fe_sq(v3), v);
-  fe r = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(u, v7)));
-  fe check = fe_mul(v, fe_sq(r));
-  const bool correct = fe_equal(check, u);
-  const bool flipped = fe_is_zero(fe_add(check, u));
-  const bool flipped_i = fe_is_zero(fe_add(check, fe_mul(u, FE_SQRTM1)));
-  r = fe_select(r, fe_mul(r, FE_SQRTM1), flipped || flipped_i);
-  r = fe_select(r, fe_neg(r), fe_is_negative(r));
-  const bool sign = (w[7] >> 31) & 1;
-  fe x = fe_select(r, fe_neg(r), sign);
-  out.X = x;
-  out.Y = y;
-  out.Z = one;
-  out.T = fe_mul(x, y);
-  fe_to_words(y, ycanon);
-  return correct || flipped;
+// The two 252-squaring exponentiations are serial chains; running A's and R's side by side gives
+// the scheduler two independent chains per lane.  Also returns the canonical y words (for the
+// small-order test).
+FE_DEV void ge_decompress2(ge_p3 out[2], const u32* const w[2], u32 ycanon[2][8], bool ok[2]) {
+  fe y[2], u[2], v[2], z[2];
+  const fe one = fe_one();
+  _Pragma("unroll") for (int k = 0; k < 2; ++k) {
+    y[k] = fe_from_words(w[k]);
+    fe yy = fe_sq(y[k]);
+    u[k] = fe_sub(yy, one);
+    v[k] = fe_add(fe_mul(yy, FE_D), one);
+    fe v3 = fe_mul(fe_sq(v[k]), v[k]);
+    fe v7 = fe_mul(fe_sq(v3), v[k]);
+    z[k] = fe_mul(u[k], v7);
+    v[k] = v3;   // keep v^3 for r = u v^3 (u v^7)^((p-5)/8); v itself is recomputed below
+  }
+  // z^(2^252 - 3) for both, interleaved
+  fe a[2], b[2], t[2];
+#define BOTH(stmt) _Pragma("unroll") for (int k = 0; k < 2; ++k) { stmt; }
+  fe z2[2], z9[2], z11[2];
+  BOTH(z2[k] = fe_sq(z[k]));
+  BOTH(t[k] = fe_sq(fe_sq(z2[k])));
+  BOTH(z9[k] = fe_mul(z[k], t[k]));
+  BOTH(z11[k] = fe_mul(z2[k], z9[k]));
+  BOTH(a[k] = fe_mul(z9[k], fe_sq(z11[k])));                 // 2^5 - 1
+  fe t10[2], t50[2];
+  BOTH(t[k] = a[k]);
+  _Pragma("unroll 1") for (int i = 0; i < 5; ++i) BOTH(t[k] = fe_sq(t[k]));
+  BOTH(t10[k] = fe_mul(t[k], a[k]));                         // 2^10 - 1
+  BOTH(t[k] = t10[k]);
+  _Pragma("unroll 1") for (int i = 0; i < 10; ++i) BOTH(t[k] = fe_sq(t[k]));
+  BOTH(b[k] = fe_mul(t[k], t10[k]));                         // 2^20 - 1
+  BOTH(t[k] = b[k]);
+  _Pragma("unroll 1") for (int i = 0; i < 20; ++i) BOTH(t[k] = fe_sq(t[k]));
+  BOTH(b[k] = fe_mul(t[k], b[k]));                           // 2^40 - 1
+  _Pragma("unroll 1") for (int i = 0; i < 10; ++i) BOTH(b[k] = fe_sq(b[k]));
+  BOTH(t50[k] = fe_mul(b[k], t10[k]));                       // 2^50 - 1
+  BOTH(t[k] = t50[k]);
+  _Pragma("unroll 1") for (int i = 0; i < 50; ++i) BOTH(t[k] = fe_sq(t[k]));
+  BOTH(b[k] = fe_mul(t[k], t50[k]));                         // 2^100 - 1
+  BOTH(t[k] = b[k]);
+  _Pragma("unroll 1") for (int i = 0; i < 100; ++i) BOTH(t[k] = fe_sq(t[k]));
+  BOTH(b[k] = fe_mul(t[k], b[k]));                           // 2^200 - 1
+  _Pragma("unroll 1") for (int i = 0; i < 50; ++i) BOTH(b[k] = fe_sq(b[k]));
+  BOTH(b[k] = fe_mul(b[k], t50[k]));                         // 2^250 - 1
+  BOTH(b[k] = fe_mul(fe_sq(fe_sq(b[k])), z[k]));             // 2^252 - 3
+#undef BOTH
+  _Pragma("unroll") for (int k = 0; k < 2; ++k) {
+    // r = u v^3 (u v^7)^((p-5)/8); check = v r^2
+    fe r = fe_mul(fe_mul(u[k], v[k]), b[k]);
+    const fe yy = fe_sq(y[k]);
+    const fe vv = fe_add(fe_mul(yy, FE_D), one);
+    fe check = fe_mul(vv, fe_sq(r));
+    const bool correct = fe_equal(check, u[k]);
+    const bool flipped = fe_is_zero(fe_add(check, u[k]));
+    const bool flipped_i = fe_is_zero(fe_add(check, fe_mul(u[k], FE_SQRTM1)));
+    r = fe_select(r, fe_mul(r, FE_SQRTM1), flipped || flipped_i);
+    r = fe_select(r, fe_neg(r), fe_is_negative(r));
+    const bool sign = (w[k][7] >> 31) & 1;
+    const fe x = fe_select(r, fe_neg(r), sign);
+    out[k].X = x;
+    out[k].Y = y[k];
+    out[k].Z = one;
+    out[k].T = fe_mul(x, y[k]);
+    fe_to_words(y[k], ycanon[k]);
+    ok[k] = correct || flipped;
+  }
 }
 
 // A decompressed point is small-order iff its y is one of the five y-coordinates of E[8]

@@ -181,8 +181,10 @@ __device__ __forceinline__ ge_p2 double_scalarmult(const LaneTable& tab, u32 kd[
   return ge_p1p1_to_p2(t);
 }
 
-__device__ __noinline__ bool decompress_point(ge_p3& out, const u32 w[8], u32 ycanon[8]) {
-  return ge_decompress(out, w, ycanon);
+__device__ __noinline__ void decompress_pair(ge_p3 out[2], const u32* a, const u32* b, u32 ycanon[2][8],
+                                             bool ok[2]) {
+  const u32* const w[2] = {a, b};
+  ge_decompress2(out, w, ycanon, ok);
 }
 
 // One verification equation (strict: dalek verify_strict; else the batch leaf).  Returns the
@@ -193,12 +195,15 @@ __device__ bool verify_one(const u32 mw[8], const u32 aw[8], const u32 sigw[16],
   _Pragma("unroll") for (int i = 0; i < 8; ++i) { rw[i] = sigw[i]; sw[i] = sigw[8 + i]; }
   const bool s_ok = sc_lt_l(sw);
 
-  ge_p3 A, R;
-  u32 ya[8], yr[8];
-  const bool a_ok = decompress_point(A, aw, ya);
+  ge_p3 AR[2];
+  u32 ycan[2][8];
+  bool okp[2];
+  decompress_pair(AR, aw, rw, ycan, okp);
+  const ge_p3& A = AR[0];
+  const ge_p3& R = AR[1];
+  const bool a_ok = okp[0], r_ok = okp[1];
   build_table(tab, ge_p3_neg(A));          // table of -A multiples
-  const bool r_ok = decompress_point(R, rw, yr);
-  const bool small = strict && (ycanon_is_small_order(ya) || ycanon_is_small_order(yr));
+  const bool small = strict && (ycanon_is_small_order(ycan[0]) || ycanon_is_small_order(ycan[1]));
 
   // k = SHA-512(R || A || M) mod l, over the raw input bytes
   uint64_t w[16];
