@@ -26,6 +26,7 @@
 #include "ge25519.h"
 #include "sc25519.h"
 #include "sha512.h"
+#include "lattice.h"
 
 namespace nwc {
 
@@ -87,17 +88,22 @@ __device__ void sha512_one_block(const u32* words, int len, u32 digest_le[16]) {
   }
 }
 
-// ------------------------------------------------------------------------------- base table
-// table[i] = i*B (i = 0..128) in affine Niels form.  One lane per entry.
+// ------------------------------------------------------------------------------- base tables
+// table[i] = i*B and table[129 + i] = i*(2^140 B), i = 0..128, affine Niels.  One lane per entry.
+constexpr int BASE_SPLIT_BITS = 140;
 __global__ void k_build_base_table(ge_niels* table) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > 128) return;
+  if (i >= 2 * 129) return;
   ge_p3 b = ge_base_point();
+  if (i >= 129) {
+    for (int k = 0; k < BASE_SPLIT_BITS; ++k) b = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(b)));
+  }
+  const int m = i % 129;
   ge_cached bc = ge_p3_to_cached(b);
   ge_p3 acc = ge_p3_identity();
   for (int bit = 7; bit >= 0; --bit) {
     acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
-    if ((i >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, bc));
+    if ((m >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, bc));
   }
   table[i] = ge_p3_to_niels(acc);
 }
@@ -140,9 +146,19 @@ __device__ __forceinline__ void build_table(const LaneTable& tab, const ge_p3& P
   }
 }
 
-// R' = k*P + s*B with P's table in `tab`, kd: radix-16 digits of k (nibble d+8), sd: radix-256
-// digits of s (byte d+128), sB: basepoint table in LDS.  Uniform schedule: every lane adds at
-// every window.  The next window's table entry is loaded while this window's doublings run.
+__device__ __forceinline__ void ladder_double4(ge_p1p1& t, ge_p3& acc) {
+  ge_p2 p2 = ge_p1p1_to_p2(t);
+  t = ge_p2_dbl(p2);
+  p2 = ge_p1p1_to_p2(t);
+  t = ge_p2_dbl(p2);
+  p2 = ge_p1p1_to_p2(t);
+  t = ge_p2_dbl(p2);
+  p2 = ge_p1p1_to_p2(t);
+  t = ge_p2_dbl(p2);
+  acc = ge_p1p1_to_p3(t);
+}
+
+// ---- full-length ladder: R' = k*P + s*B, 64 radix-16 windows (the fallback path) -------------
 __device__ __forceinline__ ge_p2 double_scalarmult(const LaneTable& tab, u32 kd[8], u32 sd[8],
                                                    const ge_niels* sB) {
   ge_p3 acc = ge_p3_identity();
@@ -158,17 +174,7 @@ __device__ __forceinline__ ge_p2 double_scalarmult(const LaneTable& tab, u32 kd[
       digits_shl(kd, 4);
       nxt = tab.load(dk < 0 ? -dk : dk);
     }
-    if (w != 63) {
-      ge_p2 p2 = ge_p1p1_to_p2(t);
-      t = ge_p2_dbl(p2);
-      p2 = ge_p1p1_to_p2(t);
-      t = ge_p2_dbl(p2);
-      p2 = ge_p1p1_to_p2(t);
-      t = ge_p2_dbl(p2);
-      p2 = ge_p1p1_to_p2(t);
-      t = ge_p2_dbl(p2);
-      acc = ge_p1p1_to_p3(t);
-    }
+    if (w != 63) ladder_double4(t, acc);
     t = ge_add_cached(acc, cur);
     if ((w & 1) == 0) {
       const i32 ds = (i32)(sd[7] >> 24) - 128;
@@ -181,31 +187,91 @@ __device__ __forceinline__ ge_p2 double_scalarmult(const LaneTable& tab, u32 kd[
   return ge_p1p1_to_p2(t);
 }
 
+// ---- half-size ladder: Q = eB*B + c'*PA + d*PR over 35 radix-16 windows (140 bits) -----------
+// cd/dd: radix-16 digits (nibble d+8) of |c| and d, digit 34 at the top of word 4;
+// el/eh: radix-256 digits (byte d+128) of eB mod 2^140 and eB >> 140, digit 17 at the top.
+constexpr int HALF_WINDOWS = 35;
+__device__ __forceinline__ void shl160(u32 d[5], int bits) {
+  _Pragma("unroll") for (int i = 4; i > 0; --i) d[i] = (d[i] << bits) | (d[i - 1] >> (32 - bits));
+  d[0] <<= bits;
+}
+
+__device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const LaneTable& tr, u32 cd[5], u32 dd[5],
+                                                 u32 el[5], u32 eh[5], const ge_niels* sB, const ge_niels* sB2) {
+  ge_p3 acc = ge_p3_identity();
+  ge_p1p1 t;
+  i32 da = (i32)(cd[4] >> 28) - 8;
+  i32 dr = (i32)(dd[4] >> 28) - 8;
+  shl160(cd, 4);
+  shl160(dd, 4);
+  ge_cached na = ta.load(da < 0 ? -da : da);
+  ge_cached nr = tr.load(dr < 0 ? -dr : dr);
+#pragma unroll 1
+  for (int w = HALF_WINDOWS - 1; w >= 0; --w) {
+    const ge_cached ca = ge_cached_cneg(na, da < 0);
+    const ge_cached cr = ge_cached_cneg(nr, dr < 0);
+    if (w > 0) {
+      da = (i32)(cd[4] >> 28) - 8;
+      dr = (i32)(dd[4] >> 28) - 8;
+      shl160(cd, 4);
+      shl160(dd, 4);
+      na = ta.load(da < 0 ? -da : da);
+      nr = tr.load(dr < 0 ? -dr : dr);
+    }
+    if (w != HALF_WINDOWS - 1) ladder_double4(t, acc);
+    t = ge_add_cached(acc, ca);
+    acc = ge_p1p1_to_p3(t);
+    t = ge_add_cached(acc, cr);
+    if ((w & 1) == 0) {
+      const i32 d0 = (i32)(el[4] >> 24) - 128;
+      const i32 d1 = (i32)(eh[4] >> 24) - 128;
+      shl160(el, 8);
+      shl160(eh, 8);
+      const ge_niels n0 = sB[d0 < 0 ? -d0 : d0];
+      acc = ge_p1p1_to_p3(t);
+      t = ge_add_niels(acc, ge_niels_cneg(n0, d0 < 0));
+      const ge_niels n1 = sB2[d1 < 0 ? -d1 : d1];
+      acc = ge_p1p1_to_p3(t);
+      t = ge_add_niels(acc, ge_niels_cneg(n1, d1 < 0));
+    }
+  }
+  return ge_p1p1_to_p2(t);
+}
+
+// Signed radix-16 digits of x < 2^138 (35 digits, d in [-8, 7]) as nibbles d+8, digit i at
+// nibble i+5 of the 5-word output (so digit 34 is the top nibble of word 4).
+__device__ __forceinline__ void recode16_35(const u32 x[5], u32 out[5]) {
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) out[i] = 0;
+  i32 carry = 0;
+  _Pragma("unroll") for (int i = 0; i < HALF_WINDOWS; ++i) {
+    i32 d = (i32)((x[i >> 3] >> (4 * (i & 7))) & 15u) + carry;
+    carry = (d + 8) >> 4;
+    d -= carry << 4;
+    const int pos = i + 5;
+    out[pos >> 3] |= (u32)(d + 8) << (4 * (pos & 7));
+  }
+}
+// Signed radix-256 digits of x < 2^140 (18 digits) as bytes d+128, digit i at byte i+2.
+__device__ __forceinline__ void recode256_18(const u32 x[5], u32 out[5]) {
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) out[i] = 0;
+  i32 carry = 0;
+  _Pragma("unroll") for (int i = 0; i < 18; ++i) {
+    i32 d = (i32)((x[i >> 2] >> (8 * (i & 3))) & 255u) + carry;
+    carry = (d + 128) >> 8;
+    d -= carry << 8;
+    const int pos = i + 2;
+    out[pos >> 2] |= (u32)(d + 128) << (8 * (pos & 3));
+  }
+}
+
 __device__ __noinline__ void decompress_pair(ge_p3 out[2], const u32* a, const u32* b, u32 ycanon[2][8],
                                              bool ok[2]) {
   const u32* const w[2] = {a, b};
   ge_decompress2(out, w, ycanon, ok);
 }
 
-// One verification equation (strict: dalek verify_strict; else the batch leaf).  Returns the
-// verdict bit.  `tab` is this lane's table slot.
-__device__ bool verify_one(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict,
-                           const ge_niels* sB, const LaneTable& tab) {
-  u32 rw[8], sw[8];
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) { rw[i] = sigw[i]; sw[i] = sigw[8 + i]; }
-  const bool s_ok = sc_lt_l(sw);
-
-  ge_p3 AR[2];
-  u32 ycan[2][8];
-  bool okp[2];
-  decompress_pair(AR, aw, rw, ycan, okp);
-  const ge_p3& A = AR[0];
-  const ge_p3& R = AR[1];
-  const bool a_ok = okp[0], r_ok = okp[1];
-  build_table(tab, ge_p3_neg(A));          // table of -A multiples
-  const bool small = strict && (ycanon_is_small_order(ycan[0]) || ycanon_is_small_order(ycan[1]));
-
-  // k = SHA-512(R || A || M) mod l, over the raw input bytes
+// k = SHA-512(R || A || M) mod l over the raw input bytes (one block: 96 bytes + padding)
+__device__ __forceinline__ void challenge(const u32 rw[8], const u32 aw[8], const u32 mw[8], u32 kw[8]) {
   uint64_t w[16];
   _Pragma("unroll") for (int i = 0; i < 4; ++i) {
     w[i] = be64_from_le32(rw[2 * i], rw[2 * i + 1]);
@@ -221,50 +287,166 @@ __device__ bool verify_one(const u32 mw[8], const u32 aw[8], const u32 sigw[16],
     hw[2 * i] = __builtin_bswap32((u32)(st[i] >> 32));
     hw[2 * i + 1] = __builtin_bswap32((u32)st[i]);
   }
-  u32 kw[8];
   sc_reduce512(hw, kw);
-  u32 kd[8], sd[8];
-  sc_recode_radix16(kw, kd);
-  sc_recode_radix256(sw, sd);
-  const ge_p2 rp = double_scalarmult(tab, kd, sd, sB);
+}
 
-  // R' == R  <=>  X' == x_R Z'  and  Y' == y_R Z'   (R affine: Z = 1)
-  const bool eq = fe_is_zero(fe_sub(rp.X, fe_mul(R.X, rp.Z))) && fe_is_zero(fe_sub(rp.Y, fe_mul(R.Y, rp.Z)));
-  return s_ok && a_ok && r_ok && !small && eq;
+// Shared prologue: parse, decode, small-order flag, challenge.
+struct Prologue {
+  ge_p3 A, R;
+  u32 kw[8], sw[8];
+  bool ok;   // s < l, A and R decode, and (strict) neither is small-order
+};
+__device__ __forceinline__ void prologue(Prologue& p, const u32 mw[8], const u32 aw[8], const u32 sigw[16],
+                                         bool strict) {
+  u32 rw[8];
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) { rw[i] = sigw[i]; p.sw[i] = sigw[8 + i]; }
+  const bool s_ok = sc_lt_l(p.sw);
+  ge_p3 AR[2];
+  u32 ycan[2][8];
+  bool okp[2];
+  decompress_pair(AR, aw, rw, ycan, okp);
+  p.A = AR[0];
+  p.R = AR[1];
+  const bool small = strict && (ycanon_is_small_order(ycan[0]) || ycanon_is_small_order(ycan[1]));
+  p.ok = s_ok && okp[0] && okp[1] && !small;
+  challenge(rw, aw, mw, p.kw);
+}
+
+// Full-length equation: R' = k(-A) + sB == R.
+__device__ bool verify_full(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels* sB,
+                            const LaneTable& tab) {
+  Prologue p;
+  prologue(p, mw, aw, sigw, strict);
+  build_table(tab, ge_p3_neg(p.A));
+  u32 kd[8], sd[8];
+  sc_recode_radix16(p.kw, kd);
+  sc_recode_radix256(p.sw, sd);
+  const ge_p2 rp = double_scalarmult(tab, kd, sd, sB);
+  const bool eq = fe_is_zero(fe_sub(rp.X, fe_mul(p.R.X, rp.Z))) && fe_is_zero(fe_sub(rp.Y, fe_mul(p.R.Y, rp.Z)));
+  return p.ok && eq;
+}
+
+// Half-size equation: [d]e = (d s mod l) B - c A - d R == O  (lattice.h).  Sets `fallback`
+// when the reduction failed; the verdict is then decided by verify_full in k_verify_fallback.
+__device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels* sB,
+                            const ge_niels* sB2, const LaneTable& ta, const LaneTable& tr, bool& fallback) {
+  Prologue p;
+  prologue(p, mw, aw, sigw, strict);
+  const lat::HalfScalars h = lat::reduce(p.kw);
+  fallback = !h.ok;
+  // eB = d * s mod l
+  u32 prod[16];
+  _Pragma("unroll") for (int i = 0; i < 16; ++i) prod[i] = 0;
+  _Pragma("unroll") for (int x = 0; x < 5; ++x) {
+    u64 carry = 0;
+    _Pragma("unroll") for (int y = 0; y < 8; ++y) {
+      const u64 tt = (u64)h.d[x] * p.sw[y] + prod[x + y] + carry;
+      prod[x + y] = (u32)tt;
+      carry = tt >> 32;
+    }
+    prod[x + 8] = (u32)carry;
+  }
+  u32 eb[8];
+  sc_reduce512(prod, eb);
+  u32 lo[5], hi[5];
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) lo[i] = eb[i];
+  lo[4] = eb[4] & ((1u << (BASE_SPLIT_BITS - 128)) - 1u);
+  _Pragma("unroll") for (int i = 0; i < 4; ++i)
+    hi[i] = (eb[4 + i] >> (BASE_SPLIT_BITS - 128)) | (i + 5 < 8 ? eb[5 + i] << (32 - (BASE_SPLIT_BITS - 128)) : 0u);
+  hi[4] = 0;
+  u32 cd[5], dd[5], el[5], eh[5];
+  recode16_35(h.c, cd);
+  recode16_35(h.d, dd);
+  recode256_18(lo, el);
+  recode256_18(hi, eh);
+  // -c A = |c| * (c < 0 ? A : -A);  -d R = d * (-R)
+  build_table(ta, h.c_neg ? p.A : ge_p3_neg(p.A));
+  build_table(tr, ge_p3_neg(p.R));
+  const ge_p2 q = half_scalarmult(ta, tr, cd, dd, el, eh, sB, sB2);
+  const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
+  return p.ok && ident && h.ok;
 }
 
 // ------------------------------------------------------------------------------- verify
 // n equations; equation i uses msgs[32 * (msg_index ? msg_index[i] : i * msg_stride)], pks[32 i],
 // sigs[64 i] (msg_stride 0 broadcasts one digest: Signature::verify_batch, crypto/src/lib.rs:214).
 // out_bits[i / 64] bit (i % 64) = verdict.  Persistent grid: block b processes 256-lane tiles
-// b, b + gridDim.x, ...; lane slot (blockIdx.x * 256 + threadIdx.x) of `scratch` holds its table.
-__global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ msgs,
-                                                const uint32_t* __restrict__ msg_index, uint64_t msg_stride,
-                                                const uint8_t* __restrict__ pks,
-                                                const uint8_t* __restrict__ sigs,
-                                                uint64_t* __restrict__ out_bits, uint64_t n,
-                                                int strict, const ge_niels* __restrict__ base_table,
-                                                uint8_t* __restrict__ scratch) {
-  __shared__ ge_niels sB[129];
-  for (int i = threadIdx.x; i < 129 * 30; i += blockDim.x)
-    reinterpret_cast<i32*>(sB)[i] = reinterpret_cast<const i32*>(base_table)[i];
+// b, b + gridDim.x, ...; lane slot (blockIdx.x * 256 + threadIdx.x) of `scratch` holds its two
+// tables.  half != 0: half-size equations; lanes whose reduction fails are appended to
+// fb_list (fb_count) and decided by k_verify_fallback.
+struct VerifyArgs {
+  const uint8_t* msgs;
+  const uint32_t* msg_index;
+  uint64_t msg_stride;
+  const uint8_t* pks;
+  const uint8_t* sigs;
+  uint64_t* out_bits;
+  uint64_t n;
+  int strict;
+  const ge_niels* base_table;   // 2 x 129 entries
+  uint8_t* scratch;             // 2 * TAB_BYTES_PER_LANE per lane slot
+  uint32_t* fb_list;
+  uint32_t* fb_count;
+  uint32_t force_fb_every;      // test hook: route equations i % every == 0 to the fallback (0 = off)
+};
+
+__device__ __forceinline__ void load_inputs(const VerifyArgs& a, uint64_t i, u32 mw[8], u32 aw[8], u32 sgw[16]) {
+  const uint64_t mi = a.msg_index ? (uint64_t)a.msg_index[i] : i * a.msg_stride;
+  load_words8(a.msgs + 32 * mi, mw);
+  load_words8(a.pks + 32 * i, aw);
+  load_words8(a.sigs + 64 * i, sgw);
+  load_words8(a.sigs + 64 * i + 32, sgw + 8);
+}
+
+__device__ __forceinline__ void stage_base_tables(const ge_niels* src, ge_niels* sB, int count) {
+  for (int i = threadIdx.x; i < count * 30; i += blockDim.x)
+    reinterpret_cast<i32*>(sB)[i] = reinterpret_cast<const i32*>(src)[i];
   __syncthreads();
-  const LaneTable tab{reinterpret_cast<uint4*>(scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) *
-                                                             TAB_BYTES_PER_LANE)};
+}
+
+template <bool HALF>
+__global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
+  __shared__ ge_niels sB[HALF ? 2 * 129 : 129];
+  stage_base_tables(a.base_table, sB, HALF ? 2 * 129 : 129);
+  const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint8_t* base = a.scratch + slot * 2 * TAB_BYTES_PER_LANE;
+  const LaneTable ta{reinterpret_cast<uint4*>(base)};
+  const LaneTable tr{reinterpret_cast<uint4*>(base + TAB_BYTES_PER_LANE)};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
-    const uint64_t i = base + threadIdx.x;
-    const bool active = i < n;
-    const uint64_t ii = active ? i : 0;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < a.n; b0 += stride) {
+    const uint64_t i = b0 + threadIdx.x;
+    const bool active = i < a.n;
     u32 mw[8], aw[8], sgw[16];
-    const uint64_t mi = msg_index ? (uint64_t)msg_index[ii] : ii * msg_stride;
-    load_words8(msgs + 32 * mi, mw);
-    load_words8(pks + 32 * ii, aw);
-    load_words8(sigs + 64 * ii, sgw);
-    load_words8(sigs + 64 * ii + 32, sgw + 8);
-    bool v = verify_one(mw, aw, sgw, strict != 0, sB, tab) && active;
+    load_inputs(a, active ? i : 0, mw, aw, sgw);
+    bool fb = false;
+    bool v;
+    if constexpr (HALF) v = verify_half(mw, aw, sgw, a.strict != 0, sB, sB + 129, ta, tr, fb);
+    else v = verify_full(mw, aw, sgw, a.strict != 0, sB, ta);
+    if (HALF && a.force_fb_every && (i % a.force_fb_every) == 0) { fb = true; v = false; }
+    v = v && active;
+    fb = fb && active;
+    if (fb) a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)i;
     const uint64_t ballot = __ballot(v);
-    if ((threadIdx.x & 63) == 0 && base + (threadIdx.x & ~63u) < n) out_bits[(base + threadIdx.x) >> 6] = ballot;
+    if ((threadIdx.x & 63) == 0 && b0 + (threadIdx.x & ~63u) < a.n) a.out_bits[(b0 + threadIdx.x) >> 6] = ballot;
+  }
+}
+
+template __global__ void k_verify<true>(VerifyArgs);
+template __global__ void k_verify<false>(VerifyArgs);
+
+// Full-length re-verification of the lanes k_verify could not reduce (rare); sets their bits.
+__global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {
+  __shared__ ge_niels sB[129];
+  stage_base_tables(a.base_table, sB, 129);
+  const uint32_t count = *a.fb_count;
+  const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const LaneTable ta{reinterpret_cast<uint4*>(a.scratch + slot * 2 * TAB_BYTES_PER_LANE)};
+  for (uint32_t j = (uint32_t)slot; j < count; j += gridDim.x * blockDim.x) {
+    const uint64_t i = a.fb_list[j];
+    u32 mw[8], aw[8], sgw[16];
+    load_inputs(a, i, mw, aw, sgw);
+    if (verify_full(mw, aw, sgw, a.strict != 0, sB, ta))
+      atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));
   }
 }
 

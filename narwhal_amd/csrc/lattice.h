@@ -1,0 +1,217 @@
+// Half-size scalars for Ed25519 verification (host + device).
+//
+// The verification equation e = sB - kA - R = O (dalek verify_strict / the batch leaf,
+// SURVEY.md A.3 step 5, A.5) needs 252 shared doublings for the 253-bit k.  Following the
+// lattice-reduction idea of Pornin ("Optimized lattice basis reduction in dimension 2, and fast
+// Schnorr and EdDSA signature verification", 2020), find (c, d) with
+//       d * k = c  (mod 8l),   d odd,   |c|, |d| < 2^138,
+// then  [d] e = (d s mod l) B - c A - d R.   Because |E| = 8l and d is odd with 0 < d < l,
+// multiplication by d is injective on E (= Z_l x Z_8), so [d] e = O  <=>  e = O: the verdict is
+// exactly dalek's, for every A and R including small/mixed-order ones (the modulus is 8l, not l,
+// so (dk - c) A = O holds for points with torsion too).  The multi-scalar multiplication then
+// needs only ~136 doublings.
+//
+// (c, d) come from the continued-fraction expansion of k / (8l) (Euclid on r_{-1} = 8l,
+// r_0 = k with cofactors t): stop at the first r_i < 2^127; if t_i is even, take the best odd
+// combination (r_{i-1} - m r_i, t_{i-1} - m t_i).  Quotients are estimated from the top 64 bits
+// in double precision and always under-estimated, so each step subtracts q <= floor(r0/r1)
+// copies and the remainder sequence is exactly Euclid's.  A lane that does not converge within
+// the iteration budget or whose candidate exceeds 2^138 reports failure and is re-verified by the
+// full-length ladder (probability ~1e-7 per signature for uniform k).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define NWC_HD __host__ __device__ __forceinline__
+#else
+#define NWC_HD static inline
+#endif
+
+namespace nwc {
+namespace lat {
+
+typedef uint32_t w32;
+typedef uint64_t w64;
+
+constexpr int HALF_BITS = 138;   // accepted |c|, |d| < 2^HALF_BITS
+constexpr int MAX_ITERS = 192;   // Euclid steps (incl. partial-quotient steps); ~70 on average
+
+// 8l, little-endian words
+NWC_HD void eight_l(w32 n[8]) {
+  const w32 L[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0u, 0u, 0u, 0x10000000u};
+  w32 carry = 0;
+  for (int i = 0; i < 8; ++i) { n[i] = (L[i] << 3) | carry; carry = L[i] >> 29; }
+}
+
+NWC_HD bool lt8(const w32 a[8], const w32 b[8]) {
+  bool lt = false, eq = true;
+  for (int i = 7; i >= 0; --i) { lt = lt || (eq && a[i] < b[i]); eq = eq && (a[i] == b[i]); }
+  return lt;
+}
+
+// a -= q * b (8 words, a >= q*b guaranteed by the caller)
+NWC_HD void submul8(w32 a[8], const w32 b[8], w32 q) {
+  w64 borrow = 0;   // amount to subtract from the next word
+  for (int i = 0; i < 8; ++i) {
+    const w64 p = (w64)q * b[i] + borrow;
+    const w32 lo = (w32)p;
+    w64 hi = p >> 32;
+    const w32 ai = a[i];
+    a[i] = ai - lo;
+    hi += (ai < lo) ? 1u : 0u;
+    borrow = hi;
+  }
+}
+
+// t -= q * u, 5-word two's complement (wraps mod 2^160; magnitudes stay < 2^159)
+NWC_HD void submul5s(w32 t[5], const w32 u[5], w32 q) {
+  w64 carry = 0;
+  w32 p[5];
+  for (int i = 0; i < 5; ++i) { w64 x = (w64)q * u[i] + carry; p[i] = (w32)x; carry = x >> 32; }
+  w64 br = 0;
+  for (int i = 0; i < 5; ++i) { w64 x = (w64)t[i] - p[i] - br; t[i] = (w32)x; br = (x >> 63) & 1; }
+}
+
+NWC_HD bool neg5(const w32 t[5]) { return (t[4] >> 31) != 0; }
+NWC_HD void abs5(const w32 t[5], w32 out[5]) {
+  const bool n = neg5(t);
+  w64 c = 1;
+  for (int i = 0; i < 5; ++i) {
+    w32 v = n ? ~t[i] : t[i];
+    if (n) { w64 x = (w64)v + c; v = (w32)x; c = x >> 32; }
+    out[i] = v;
+  }
+}
+NWC_HD int bitlen5(const w32 a[5]) {
+  int b = 0;
+  for (int i = 0; i < 5; ++i) if (a[i]) b = 32 * i + 32 - __builtin_clz(a[i]);
+  return b;
+}
+NWC_HD int bitlen8(const w32 a[8]) {
+  int b = 0;
+  for (int i = 0; i < 8; ++i) if (a[i]) b = 32 * i + 32 - __builtin_clz(a[i]);
+  return b;
+}
+
+// Top 64 bits of a and b at a's top word j (b <= a): floor(a'/(b'+1)) <= floor(a/b), >= 1.
+NWC_HD w32 quot_est(const w32 a[8], const w32 b[8]) {
+  int j = 1;
+  for (int i = 1; i < 8; ++i) if (a[i]) j = i;
+  w32 ah = 0, al = 0, bh = 0, bl = 0;
+  for (int i = 1; i < 8; ++i) {
+    if (i == j) { ah = a[i]; al = a[i - 1]; bh = b[i]; bl = b[i - 1]; }
+  }
+  const w64 A = ((w64)ah << 32) | al;
+  const w64 B = ((w64)bh << 32) | bl;
+  // exact-in-double operands: A truncated to 53 bits, B rounded up to 53 bits (+1)
+  const w64 As = A >> 11, Bs = (B >> 11) + 1;
+  double q = (double)As / (double)Bs;
+  q = q * (1.0 - 1.0 / 4503599627370496.0);   // 1 - 2^-52: never round up across an integer
+  w32 qi;
+  if (q >= 4294967295.0) qi = 0xFFFFFFFFu;
+  else qi = (w32)q;
+  return qi < 1 ? 1u : qi;
+}
+
+// Result of the reduction.  ok == false -> use the full-length ladder.
+struct HalfScalars {
+  w32 c[5];      // |c|
+  w32 d[5];      // d > 0, odd
+  bool c_neg;    // c < 0
+  bool ok;
+};
+
+NWC_HD HalfScalars reduce(const w32 k[8]) {
+  w32 r0[8], r1[8], t0[5], t1[5];
+  eight_l(r0);
+  for (int i = 0; i < 8; ++i) r1[i] = k[i];
+  for (int i = 0; i < 5; ++i) { t0[i] = 0; t1[i] = 0; }
+  t1[0] = 1;
+  bool done = false;
+  for (int it = 0; it < MAX_ITERS; ++it) {
+    // stop at the first r1 < 2^127
+    done = (r1[7] | r1[6] | r1[5] | r1[4]) == 0 && r1[3] < 0x80000000u;
+    if (done) break;
+    const w32 q = quot_est(r0, r1);
+    submul8(r0, r1, q);
+    submul5s(t0, t1, q);
+    if (lt8(r0, r1)) {
+      for (int i = 0; i < 8; ++i) { w32 x = r0[i]; r0[i] = r1[i]; r1[i] = x; }
+      for (int i = 0; i < 5; ++i) { w32 x = t0[i]; t0[i] = t1[i]; t1[i] = x; }
+    }
+  }
+  HalfScalars h;
+  h.ok = done;
+  // candidate 1: (r1, t1) if t1 odd; else the best odd (r0 - m r1, t0 - m t1)
+  w32 c8[8], tc[5];
+  if (t1[0] & 1) {
+    for (int i = 0; i < 8; ++i) c8[i] = r1[i];
+    for (int i = 0; i < 5; ++i) tc[i] = t1[i];
+  } else {
+    // m ~ (r0 - |t0|) / (r1 + |t1|), estimated in double from the top bits
+    w32 a0[5], a1[5];
+    abs5(t0, a0);
+    abs5(t1, a1);
+    auto approx8 = [](const w32 x[8]) -> double {
+      double v = 0; for (int i = 7; i >= 0; --i) v = v * 4294967296.0 + (double)x[i]; return v; };
+    auto approx5 = [](const w32 x[5]) -> double {
+      double v = 0; for (int i = 4; i >= 0; --i) v = v * 4294967296.0 + (double)x[i]; return v; };
+    const double num = approx8(r0) - approx5(a0);
+    const double den = approx8(r1) + approx5(a1);
+    double mf = den > 0 ? num / den : 0.0;
+    if (!(mf > 0)) mf = 0;
+    if (mf > 4294967294.0) mf = 4294967294.0;
+    w32 m = (w32)mf;
+    // try m and m + 1, keep the smaller max bit length
+    w32 best_c[8], best_t[5];
+    int best_bits = 1 << 20;
+    for (int dm = 0; dm < 2; ++dm) {
+      const w32 mm = m + (w32)dm;
+      w32 cc[8], tt[5];
+      for (int i = 0; i < 8; ++i) cc[i] = r0[i];
+      for (int i = 0; i < 5; ++i) tt[i] = t0[i];
+      // cc = r0 - mm r1 (may exceed r0's range only if mm r1 > r0: then skip)
+      bool valid = true;
+      {
+        // compute mm * r1 and compare with r0
+        w32 p[9]; w64 carry = 0;
+        for (int i = 0; i < 8; ++i) { w64 x = (w64)mm * r1[i] + carry; p[i] = (w32)x; carry = x >> 32; }
+        p[8] = (w32)carry;
+        if (p[8]) valid = false;
+        else {
+          bool lt = false, eq = true;
+          for (int i = 7; i >= 0; --i) { lt = lt || (eq && r0[i] < p[i]); eq = eq && (r0[i] == p[i]); }
+          if (lt) valid = false;
+        }
+      }
+      // |t0 - mm t1| = |t0| + mm |t1| must stay far below 2^159 (no wrap of the 160-bit t)
+      if (bitlen5(a1) + (32 - __builtin_clz(mm | 1u)) > 150) valid = false;
+      if (!valid) continue;
+      submul8(cc, r1, mm);
+      submul5s(tt, t1, mm);
+      w32 at[5]; abs5(tt, at);
+      int bits = bitlen8(cc); const int tb = bitlen5(at); if (tb > bits) bits = tb;
+      if (bits < best_bits) {
+        best_bits = bits;
+        for (int i = 0; i < 8; ++i) best_c[i] = cc[i];
+        for (int i = 0; i < 5; ++i) best_t[i] = tt[i];
+      }
+    }
+    if (best_bits == (1 << 20)) { h.ok = false; for (int i = 0; i < 8; ++i) best_c[i] = 0; for (int i = 0; i < 5; ++i) best_t[i] = 1; }
+    for (int i = 0; i < 8; ++i) c8[i] = best_c[i];
+    for (int i = 0; i < 5; ++i) tc[i] = best_t[i];
+  }
+  // sign-normalise: d > 0.  c = c8 (>= 0) times sign(t).
+  const bool tneg = neg5(tc);
+  abs5(tc, h.d);
+  h.c_neg = tneg;     // (c, d) -> (-c, -d) when d < 0; c8 >= 0, so then c < 0
+  for (int i = 0; i < 5; ++i) h.c[i] = c8[i];
+  const bool c_small = (c8[5] | c8[6] | c8[7]) == 0 && bitlen5(h.c) <= HALF_BITS;
+  const bool d_small = bitlen5(h.d) <= HALF_BITS;
+  if (!(c_small && d_small)) h.ok = false;
+  if (c8[0] == 0 && c8[1] == 0 && c8[2] == 0 && c8[3] == 0 && c8[4] == 0) h.c_neg = false;
+  return h;
+}
+
+}  // namespace lat
+}  // namespace nwc

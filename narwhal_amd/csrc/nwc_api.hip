@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -54,6 +55,9 @@ struct DevCtx {
   // serialised across streams with `scratch_free` (recorded after each such launch).
   uint8_t* scratch = nullptr;
   size_t scratch_cap = 0;
+  uint32_t* fb_list = nullptr;     // lanes whose half-size reduction failed (k_verify_fallback)
+  uint32_t* fb_count = nullptr;
+  size_t fb_cap = 0;
   hipEvent_t scratch_free = nullptr;
   uint8_t* arena = nullptr;
   size_t arena_cap = 0;
@@ -91,10 +95,11 @@ int init_device(DevCtx& d) {
   HIP_TRY(hipEventCreateWithFlags(&d.scratch_free, hipEventDisableTiming));
   d.cus = prop.multiProcessorCount;
   int bpc = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify), 256, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify<true>), 256, 0));
   d.verify_blocks_per_cu = bpc > 0 ? bpc : 1;
-  HIP_TRY(hipMalloc(&d.base_table, 129 * sizeof(nwc::ge_niels)));
-  hipLaunchKernelGGL(nwc::k_build_base_table, dim3(3), dim3(64), 0, d.stream, d.base_table);
+  HIP_TRY(hipMalloc(&d.base_table, 2 * 129 * sizeof(nwc::ge_niels)));
+  HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
+  hipLaunchKernelGGL(nwc::k_build_base_table, dim3(5), dim3(64), 0, d.stream, d.base_table);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(d.stream));
   return 0;
@@ -111,6 +116,16 @@ int require_init() {
 }
 
 // ---- launch helpers (caller holds the device mutex and has set the device) -----------------
+// Verification path: half-size equations with full-length fallback (default), or the
+// full-length ladder for every lane (NWC_VERIFY_PATH=full; used to cross-check the two paths).
+bool half_path() {
+  static const bool half = [] {
+    const char* e = std::getenv("NWC_VERIFY_PATH");
+    return !(e && std::strcmp(e, "full") == 0);
+  }();
+  return half;
+}
+
 int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
                   hipStream_t s) {
@@ -119,20 +134,43 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   // persistent grid: a few blocks per resident slot so the tail is short
   const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * 4;
   const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
-  const size_t need = (size_t)grid * 256 * nwc::TAB_BYTES_PER_LANE;
-  if (need > d.scratch_cap) {
+  const size_t per_lane = 2 * nwc::TAB_BYTES_PER_LANE;
+  if ((size_t)grid * 256 * per_lane > d.scratch_cap || n > d.fb_cap) {
     HIP_TRY(hipEventSynchronize(d.scratch_free));
-    if (d.scratch) HIP_TRY(hipFree(d.scratch));
-    d.scratch = nullptr;
-    d.scratch_cap = 0;
-    const size_t full = (size_t)cap * 256 * nwc::TAB_BYTES_PER_LANE;
-    HIP_TRY(hipMalloc(&d.scratch, full));
-    d.scratch_cap = full;
+    if ((size_t)grid * 256 * per_lane > d.scratch_cap) {
+      if (d.scratch) HIP_TRY(hipFree(d.scratch));
+      d.scratch = nullptr;
+      d.scratch_cap = 0;
+      const size_t full = (size_t)cap * 256 * per_lane;
+      HIP_TRY(hipMalloc(&d.scratch, full));
+      d.scratch_cap = full;
+    }
+    if (n > d.fb_cap) {
+      if (d.fb_list) HIP_TRY(hipFree(d.fb_list));
+      d.fb_list = nullptr;
+      d.fb_cap = 0;
+      const size_t c = n + n / 2 + 4096;
+      HIP_TRY(hipMalloc(&d.fb_list, 4 * c));
+      d.fb_cap = c;
+    }
   }
   HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
-  hipLaunchKernelGGL(nwc::k_verify, dim3(grid), dim3(256), 0, s, msgs, msg_index, msg_stride, pks, sigs,
-                     out_words, n, strict, d.base_table, d.scratch);
+  static const uint32_t force_every = [] {
+    const char* e = std::getenv("NWC_FORCE_FALLBACK_EVERY");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+  }();
+  nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.scratch,
+                    d.fb_list, d.fb_count, force_every};
+  const bool half = half_path();
+  if (half) HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
+  if (half) hipLaunchKernelGGL(nwc::k_verify<true>, dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(nwc::k_verify<false>, dim3(grid), dim3(256), 0, s, a);
   HIP_TRY(hipGetLastError());
+  if (half) {
+    const unsigned fgrid = grid < (unsigned)d.cus ? grid : (unsigned)d.cus;
+    hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(fgrid), dim3(256), 0, s, a);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipEventRecord(d.scratch_free, s));
   return 0;
 }
@@ -266,6 +304,8 @@ void nwc_shutdown(void) {
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     if (d->arena) (void)hipFree(d->arena);
     if (d->scratch) (void)hipFree(d->scratch);
+    if (d->fb_list) (void)hipFree(d->fb_list);
+    if (d->fb_count) (void)hipFree(d->fb_count);
     if (d->scratch_free) (void)hipEventDestroy(d->scratch_free);
     if (d->base_table) (void)hipFree(d->base_table);
     if (d->stream) (void)hipStreamDestroy(d->stream);
