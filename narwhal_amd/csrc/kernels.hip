@@ -198,44 +198,61 @@ __device__ __forceinline__ void shl160(u32 d[5], int bits) {
 
 __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const LaneTable& tr, u32 cd[5], u32 dd[5],
                                                  u32 el[5], u32 eh[5], const ge_niels* sB, const ge_niels* sB2) {
+  // Code-size discipline: the window body holds ONE doubling, ONE cached add and ONE Niels add
+  // (each in a rolled loop) so the hot loop (~30 KB) stays inside the instruction cache; fully
+  // inlined it was ~77 KB.  Each add leaves the accumulator in extended form; the next window's
+  // doublings start from its (X:Y:Z).
   ge_p3 acc = ge_p3_identity();
-  ge_p1p1 t;
+  // Entries for the current window are loaded at the end of the previous window, so their
+  // latency hides behind this window's doublings and only 80 registers are in flight.
   i32 da = (i32)(cd[4] >> 28) - 8;
   i32 dr = (i32)(dd[4] >> 28) - 8;
   shl160(cd, 4);
   shl160(dd, 4);
-  ge_cached na = ta.load(da < 0 ? -da : da);
-  ge_cached nr = tr.load(dr < 0 ? -dr : dr);
+  ge_cached ea = ta.load(da < 0 ? -da : da);
+  ge_cached er = tr.load(dr < 0 ? -dr : dr);
 #pragma unroll 1
   for (int w = HALF_WINDOWS - 1; w >= 0; --w) {
-    const ge_cached ca = ge_cached_cneg(na, da < 0);
-    const ge_cached cr = ge_cached_cneg(nr, dr < 0);
+    if (w != HALF_WINDOWS - 1) {
+      ge_p2 p2 = ge_p3_to_p2(acc);
+      ge_p1p1 t;
+#pragma unroll 1
+      for (int j = 0; j < 3; ++j) { t = ge_p2_dbl(p2); p2 = ge_p1p1_to_p2(t); }
+      t = ge_p2_dbl(p2);
+      acc = ge_p1p1_to_p3(t);
+    }
+#pragma unroll 1
+    for (int side = 0; side < 2; ++side) {
+      const bool neg = side ? (dr < 0) : (da < 0);
+      ge_cached q;
+      q.YpX = fe_select(ea.YpX, er.YpX, side != 0);
+      q.YmX = fe_select(ea.YmX, er.YmX, side != 0);
+      q.Z = fe_select(ea.Z, er.Z, side != 0);
+      q.T2d = fe_select(ea.T2d, er.T2d, side != 0);
+      acc = ge_p1p1_to_p3(ge_add_cached(acc, ge_cached_cneg(q, neg)));
+    }
     if (w > 0) {
       da = (i32)(cd[4] >> 28) - 8;
       dr = (i32)(dd[4] >> 28) - 8;
       shl160(cd, 4);
       shl160(dd, 4);
-      na = ta.load(da < 0 ? -da : da);
-      nr = tr.load(dr < 0 ? -dr : dr);
+      ea = ta.load(da < 0 ? -da : da);
+      er = tr.load(dr < 0 ? -dr : dr);
     }
-    if (w != HALF_WINDOWS - 1) ladder_double4(t, acc);
-    t = ge_add_cached(acc, ca);
-    acc = ge_p1p1_to_p3(t);
-    t = ge_add_cached(acc, cr);
     if ((w & 1) == 0) {
       const i32 d0 = (i32)(el[4] >> 24) - 128;
       const i32 d1 = (i32)(eh[4] >> 24) - 128;
       shl160(el, 8);
       shl160(eh, 8);
-      const ge_niels n0 = sB[d0 < 0 ? -d0 : d0];
-      acc = ge_p1p1_to_p3(t);
-      t = ge_add_niels(acc, ge_niels_cneg(n0, d0 < 0));
-      const ge_niels n1 = sB2[d1 < 0 ? -d1 : d1];
-      acc = ge_p1p1_to_p3(t);
-      t = ge_add_niels(acc, ge_niels_cneg(n1, d1 < 0));
+#pragma unroll 1
+      for (int side = 0; side < 2; ++side) {
+        const i32 dd_ = side ? d1 : d0;
+        const ge_niels nb = (side ? sB2 : sB)[dd_ < 0 ? -dd_ : dd_];
+        acc = ge_p1p1_to_p3(ge_add_niels(acc, ge_niels_cneg(nb, dd_ < 0)));
+      }
     }
   }
-  return ge_p1p1_to_p2(t);
+  return ge_p3_to_p2(acc);
 }
 
 // Signed radix-16 digits of x < 2^138 (35 digits, d in [-8, 7]) as nibbles d+8, digit i at
@@ -404,8 +421,11 @@ __device__ __forceinline__ void stage_base_tables(const ge_niels* src, ge_niels*
   __syncthreads();
 }
 
+#ifndef NWC_VERIFY_WAVES_PER_SIMD
+#define NWC_VERIFY_WAVES_PER_SIMD 2
+#endif
 template <bool HALF>
-__global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
+__global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(VerifyArgs a) {
   __shared__ ge_niels sB[HALF ? 2 * 129 : 129];
   stage_base_tables(a.base_table, sB, HALF ? 2 * 129 : 129);
   const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
