@@ -94,19 +94,32 @@ NWC_HD int bitlen8(const w32 a[8]) {
 }
 
 // Top 64 bits of a and b at a's top word j (b <= a): floor(a'/(b'+1)) <= floor(a/b), >= 1.
+// Branch-free: inside the loop a >= 2^127, so j is one of 3..7 (select chain, no divergence).
+NWC_HD double rcp_nr(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(x);
+  r = r * (2.0 - x * r);   // Newton: relative error ~ e0^2
+  r = r * (2.0 - x * r);
+  return r;
+#else
+  return 1.0 / x;
+#endif
+}
 NWC_HD w32 quot_est(const w32 a[8], const w32 b[8]) {
-  int j = 1;
-  for (int i = 1; i < 8; ++i) if (a[i]) j = i;
-  w32 ah = 0, al = 0, bh = 0, bl = 0;
-  for (int i = 1; i < 8; ++i) {
-    if (i == j) { ah = a[i]; al = a[i - 1]; bh = b[i]; bl = b[i - 1]; }
+  w32 ah = a[7], al = a[6], bh = b[7], bl = b[6];
+  for (int i = 6; i >= 3; --i) {
+    const bool z = ah == 0;
+    ah = z ? a[i] : ah;
+    al = z ? a[i - 1] : al;
+    bh = z ? b[i] : bh;
+    bl = z ? b[i - 1] : bl;
   }
   const w64 A = ((w64)ah << 32) | al;
   const w64 B = ((w64)bh << 32) | bl;
-  // exact-in-double operands: A truncated to 53 bits, B rounded up to 53 bits (+1)
+  // exact-in-double operands: A truncated to 53 bits, B rounded up to 53 bits (+1); the
+  // quotient is scaled by (1 - 2^-40) so reciprocal/rounding error never rounds it up.
   const w64 As = A >> 11, Bs = (B >> 11) + 1;
-  double q = (double)As / (double)Bs;
-  q = q * (1.0 - 1.0 / 4503599627370496.0);   // 1 - 2^-52: never round up across an integer
+  double q = (double)As * rcp_nr((double)Bs) * (1.0 - 1.0 / 1099511627776.0);
   w32 qi;
   if (q >= 4294967295.0) qi = 0xFFFFFFFFu;
   else qi = (w32)q;
