@@ -141,6 +141,80 @@ def cfg4_host_batch(b: int) -> bytes:
     return bytes(out)
 
 
+def bench_cfg1(lib, calls: int = 2000):
+    """BASELINE config 1: Signature::verify_batch on a 4-node certificate (3 votes, 32-byte
+    digest) through the host ABI (H2D + kernel + D2H per call).  Latency-bound by design."""
+    from narwhal_amd import _lib, device
+    import torch
+    n = 3
+    seeds = device.derive32(b"nw-cfg1-key", 0, n)
+    digest = device.derive32(b"nw-cfg1-digest", 0, 1)
+    pks, sigs = device.keygen_sign(seeds, digest.repeat(n, 1))
+    torch.cuda.synchronize()
+    d, p, s = (t.cpu().numpy().tobytes() for t in (digest, pks, sigs))
+    lat = []
+    for i in range(calls + 50):
+        t0 = time.perf_counter()
+        rc = lib.nwc_verify_batch(_lib.buf(d), _lib.buf(p), _lib.buf(s), n, None)
+        dt = time.perf_counter() - t0
+        assert rc == 0, rc
+        if i >= 50:
+            lat.append(dt)
+    lat = np.array(lat) * 1e6
+    return {"workload": "cfg1: verify_batch, 3 votes, host ABI incl. H2D/D2H", "calls": calls,
+            "p50_us": float(np.percentile(lat, 50)), "p99_us": float(np.percentile(lat, 99)),
+            "calls_per_s": float(1e6 / lat.mean())}
+
+
+def bench_cfg3(lib, m: int, steps: int):
+    """BASELINE config 3: 100-node committee, m certificates x 67 votes (quorum 2N/3+1,
+    config/src/lib.rs:181-186), each vote invalid with p = 0.01 (signed over another digest).
+    Leaf equations for every vote + per-certificate AND; bad-vote sets checked against the
+    construction.  Timed with and without the committee key cache."""
+    from narwhal_amd import _lib, device
+    import torch
+    N, Q = 100, 67
+    nv = m * Q
+    cseeds = device.derive32(b"nw-committee", 0, N)
+    cdig = device.derive32(b"nw-cert", 0, m)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x4E57)
+    voters = torch.rand((m, N), device="cuda", generator=g).argsort(dim=1)[:, :Q].reshape(-1)
+    bad = torch.rand(nv, device="cuda", generator=g) < 0.01
+    msg_index = torch.arange(m, device="cuda", dtype=torch.int32).repeat_interleave(Q)
+    signed = cdig[msg_index.long()].clone()
+    signed[bad, 0] ^= 1
+    pks, sigs = device.keygen_sign(cseeds[voters], signed)
+    offs = (torch.arange(m + 1, device="cuda", dtype=torch.int32) * Q)
+    committee_pks, _ = device.keygen_sign(cseeds, cdig[:N])
+    torch.cuda.synchronize()
+    out = {}
+    for tag, use_cache in (("no_cache", False), ("cache", True)):
+        if use_cache:
+            cpk = committee_pks.cpu().numpy()
+            _lib.check(lib.nwc_set_committee(_lib.buf(cpk), N))
+        words = torch.empty(device.words_for(nv), dtype=torch.int64, device="cuda")
+        run = lambda: device.cert_reduce(device.verify(cdig, pks, sigs, strict=False, msg_index=msg_index,  # noqa
+                                                       out=words), offs, nv)
+        run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            cw, bw = run()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        got_bad = torch.from_numpy(device.unpack_bits(bw, nv)).cuda()
+        ok = bool((got_bad == bad).all())
+        cert_ok = torch.from_numpy(device.unpack_bits(cw, m)).cuda()
+        ok = ok and bool((cert_ok == ~bad.view(m, Q).any(dim=1)).all())
+        out[tag] = {"votes_per_s": nv / dt, "certs_per_s": m / dt, "ms_per_step": dt * 1e3, "parity_ok": ok}
+    _lib.check(lib.nwc_set_committee(None, 0))
+    out["workload"] = "cfg3: %d certificates x %d votes, 1%% invalid, leaf equations + certificate AND + bad-vote set" % (m, Q)
+    out["bad_votes"] = int(bad.sum().item())
+    out["failing_certs"] = int(bad.view(m, Q).any(dim=1).sum().item())
+    return out
+
+
 # ---- timing ----------------------------------------------------------------------------------
 def timed_kernel(fn, iters: int):
     """Average duration (ms) of fn() launches measured with HIP events on torch's current
@@ -213,12 +287,14 @@ def main():
     ap.add_argument("--digest-pool", type=int, default=16384, help="distinct batches resident in HBM")
     ap.add_argument("--digest-steps", type=int, default=1)
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU-baseline leg (0 = skip)")
+    ap.add_argument("--cfg3-certs", type=int, default=100000, help="config 3 certificates (0 = skip)")
+    ap.add_argument("--cfg1-calls", type=int, default=2000, help="config 1 latency calls (0 = skip)")
     args = ap.parse_args()
 
     import torch
     rank, world, local = dist_setup(args)
     from narwhal_amd import _lib, device
-    _lib.load(device_mask=1 << local)   # the library drives the same GPU as this rank
+    lib = _lib.load(device_mask=1 << local)   # the library drives the same GPU as this rank
 
     # ---------------- verify leg (headline)
     n = args.n
@@ -279,6 +355,12 @@ def main():
                   "hbm_frac": dk_gbs / HBM_PEAK_GBS,
                   "valu_frac": dk_gbs * 1e9 / 128 * OPS_SHA / (VALU_PEAK_TOPS * 1e12)}
 
+    extras = {}
+    if world == 1 and args.cfg3_certs > 0:
+        extras["cfg3"] = bench_cfg3(lib, args.cfg3_certs, max(1, args.steps // 2))
+    if world == 1 and args.cfg1_calls > 0:
+        extras["cfg1"] = bench_cfg1(lib, args.cfg1_calls)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         cpu = cpu_baseline_verify(msgs, pks, sigs, args.cpu_budget)
@@ -304,6 +386,7 @@ def main():
                                        "(%d, %d, %d) VALU lane-ops" % (W_S, W_M, W_SHA, OPS_S, OPS_M, OPS_SHA)},
             "cpu_baseline": cpu,
             "digest": digest,
+            "configs": extras,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

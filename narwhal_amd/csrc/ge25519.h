@@ -100,16 +100,17 @@ FE_DEV ge_niels ge_niels_cneg(const ge_niels& q, bool neg) {
   return r;
 }
 
-// curve25519-dalek CompressedEdwardsY::decompress of TWO encodings at once:
+// curve25519-dalek CompressedEdwardsY::decompress of N (1 or 2) encodings at once:
 //   y = low 255 bits (y >= p accepted), u = y^2 - 1, v = d y^2 + 1, (ok, x) = sqrt_ratio_i(u, v),
 //   x := -x if the sign bit is set -- even when x == 0.
 // The two 252-squaring exponentiations are serial chains; running A's and R's side by side gives
 // the scheduler two independent chains per lane.  Also returns the canonical y words (for the
 // small-order test).
-FE_DEV void ge_decompress2(ge_p3 out[2], const u32* const w[2], u32 ycanon[2][8], bool ok[2]) {
-  fe y[2], u[2], v[2], z[2];
+template <int N>
+FE_DEV void ge_decompressN(ge_p3 out[N], const u32* const w[N], u32 ycanon[N][8], bool ok[N]) {
+  fe y[N], u[N], v[N], z[N];
   const fe one = fe_one();
-  _Pragma("unroll") for (int k = 0; k < 2; ++k) {
+  _Pragma("unroll") for (int k = 0; k < N; ++k) {
     y[k] = fe_from_words(w[k]);
     fe yy = fe_sq(y[k]);
     u[k] = fe_sub(yy, one);
@@ -120,15 +121,15 @@ FE_DEV void ge_decompress2(ge_p3 out[2], const u32* const w[2], u32 ycanon[2][8]
     v[k] = v3;   // keep v^3 for r = u v^3 (u v^7)^((p-5)/8); v itself is recomputed below
   }
   // z^(2^252 - 3) for both, interleaved
-  fe a[2], b[2], t[2];
-#define BOTH(stmt) _Pragma("unroll") for (int k = 0; k < 2; ++k) { stmt; }
-  fe z2[2], z9[2], z11[2];
+  fe a[N], b[N], t[N];
+#define BOTH(stmt) _Pragma("unroll") for (int k = 0; k < N; ++k) { stmt; }
+  fe z2[N], z9[N], z11[N];
   BOTH(z2[k] = fe_sq(z[k]));
   BOTH(t[k] = fe_sq(fe_sq(z2[k])));
   BOTH(z9[k] = fe_mul(z[k], t[k]));
   BOTH(z11[k] = fe_mul(z2[k], z9[k]));
   BOTH(a[k] = fe_mul(z9[k], fe_sq(z11[k])));                 // 2^5 - 1
-  fe t10[2], t50[2];
+  fe t10[N], t50[N];
   BOTH(t[k] = a[k]);
   _Pragma("unroll 1") for (int i = 0; i < 5; ++i) BOTH(t[k] = fe_sq(t[k]));
   BOTH(t10[k] = fe_mul(t[k], a[k]));                         // 2^10 - 1
@@ -150,7 +151,7 @@ FE_DEV void ge_decompress2(ge_p3 out[2], const u32* const w[2], u32 ycanon[2][8]
   BOTH(b[k] = fe_mul(b[k], t50[k]));                         // 2^250 - 1
   BOTH(b[k] = fe_mul(fe_sq(fe_sq(b[k])), z[k]));             // 2^252 - 3
 #undef BOTH
-  _Pragma("unroll") for (int k = 0; k < 2; ++k) {
+  _Pragma("unroll") for (int k = 0; k < N; ++k) {
     // r = u v^3 (u v^7)^((p-5)/8); check = v r^2
     fe r = fe_mul(fe_mul(u[k], v[k]), b[k]);
     const fe yy = fe_sq(y[k]);

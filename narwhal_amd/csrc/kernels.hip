@@ -108,6 +108,63 @@ __global__ void k_build_base_table(ge_niels* table) {
   table[i] = ge_p3_to_niels(acc);
 }
 
+// ------------------------------------------------------------------------------- committee cache
+// nwc_set_committee (config/src/lib.rs:154-156 Committee): per key its decode flags and the
+// 129-entry affine Niels table of j * (-A), j = 0..128, resident in L2 (15.5 KB per key).
+// Lookup is by exact 32-byte match through an open-addressing hash table built by the host, so
+// verdicts never depend on the cache: a cached key has the same decode / small-order flags and
+// the same points as decoding it per equation.
+struct Committee {
+  const u32* keys;          // n x 8 words: the raw 32-byte keys
+  const u32* flags;         // n: bit0 = decodes, bit1 = small-order
+  const ge_niels* tables;   // n x 129
+  const int32_t* slots;     // hash slot -> key index, -1 = empty
+  u32 slot_mask;            // slots - 1 (power of two)
+  u32 n;
+};
+constexpr int COMMITTEE_MAX_PROBE = 16;
+__host__ __device__ __forceinline__ u32 committee_hash(const u32 w0, const u32 w1) {
+  return (w0 * 0x9E3779B1u) ^ (w1 * 0x85EBCA77u);
+}
+__device__ __forceinline__ int committee_lookup(const Committee& c, const u32 aw[8]) {
+  if (c.n == 0) return -1;
+  const u32 h = committee_hash(aw[0], aw[1]);
+  int found = -1;
+  for (int p = 0; p < COMMITTEE_MAX_PROBE; ++p) {
+    const int idx = c.slots[(h + p) & c.slot_mask];
+    if (idx < 0) break;
+    const u32* k = c.keys + 8 * idx;
+    u32 diff = 0;
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) diff |= k[i] ^ aw[i];
+    if (diff == 0) { found = idx; break; }
+  }
+  return found;
+}
+
+// One lane per (key, j): table[key][j] = j * (-A_key); lane j == 0 also writes the flags.
+__global__ void k_build_key_tables(const u32* __restrict__ keys, u32 n, ge_niels* __restrict__ tables,
+                                   u32* __restrict__ flags) {
+  const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * 129) return;
+  const u32 key = t / 129, j = t % 129;
+  u32 w[8];
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) w[i] = keys[8 * key + i];
+  ge_p3 A[1];
+  u32 yc[1][8];
+  bool ok[1];
+  const u32* const wp[1] = {w};
+  ge_decompressN<1>(A, wp, yc, ok);
+  const ge_p3 na = ge_p3_neg(A[0]);
+  const ge_cached nc = ge_p3_to_cached(na);
+  ge_p3 acc = ge_p3_identity();
+  for (int bit = 7; bit >= 0; --bit) {
+    acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
+    if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, nc));
+  }
+  tables[(size_t)key * 129 + j] = ge_p3_to_niels(acc);
+  if (j == 0) flags[key] = (ok[0] ? 1u : 0u) | (ycanon_is_small_order(yc[0]) ? 2u : 0u);
+}
+
 // ------------------------------------------------------------------------------- ladder
 // Per-lane table of the variable base in global scratch, lane-contiguous: 9 entries x 160 B
 // (cached point = 40 dwords = 10 x dwordx4).  A lookup reads one lane's 160 contiguous bytes,
@@ -255,6 +312,64 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
   return ge_p3_to_p2(acc);
 }
 
+// Half-size ladder with a cached key: Q = eB*B + c'*(-A) + d*(-R) where the A term uses the key's
+// radix-256 Niels table (18 adds at even windows, no per-equation table or decompression).
+// ca: radix-256 digits of |c| (byte d+128, digit 17 at the top); c_neg flips every A entry.
+__device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, u32 dd[5], u32 ca[5], bool c_neg,
+                                                        const ge_niels* key_tab, u32 el[5], u32 eh[5],
+                                                        const ge_niels* sB, const ge_niels* sB2) {
+  ge_p3 acc = ge_p3_identity();
+  i32 dr = (i32)(dd[4] >> 28) - 8;
+  shl160(dd, 4);
+  ge_cached er = tr.load(dr < 0 ? -dr : dr);
+  i32 dA = (i32)(ca[4] >> 24) - 128;
+  shl160(ca, 8);
+  ge_niels ean = key_tab[dA < 0 ? -dA : dA];
+#pragma unroll 1
+  for (int w = HALF_WINDOWS - 1; w >= 0; --w) {
+    if (w != HALF_WINDOWS - 1) {
+      ge_p2 p2 = ge_p3_to_p2(acc);
+      ge_p1p1 t;
+#pragma unroll 1
+      for (int j = 0; j < 3; ++j) { t = ge_p2_dbl(p2); p2 = ge_p1p1_to_p2(t); }
+      t = ge_p2_dbl(p2);
+      acc = ge_p1p1_to_p3(t);
+    }
+    acc = ge_p1p1_to_p3(ge_add_cached(acc, ge_cached_cneg(er, dr < 0)));
+    if (w > 0) {
+      dr = (i32)(dd[4] >> 28) - 8;
+      shl160(dd, 4);
+      er = tr.load(dr < 0 ? -dr : dr);
+    }
+    if ((w & 1) == 0) {
+      const i32 d0 = (i32)(el[4] >> 24) - 128;
+      const i32 d1 = (i32)(eh[4] >> 24) - 128;
+      shl160(el, 8);
+      shl160(eh, 8);
+#pragma unroll 1
+      for (int side = 0; side < 3; ++side) {
+        ge_niels nb;
+        bool neg;
+        if (side == 0) {
+          nb = ean;
+          neg = (dA < 0) != c_neg;
+        } else {
+          const i32 dd_ = side == 1 ? d0 : d1;
+          nb = (side == 1 ? sB : sB2)[dd_ < 0 ? -dd_ : dd_];
+          neg = dd_ < 0;
+        }
+        acc = ge_p1p1_to_p3(ge_add_niels(acc, ge_niels_cneg(nb, neg)));
+      }
+      if (w > 0) {
+        dA = (i32)(ca[4] >> 24) - 128;
+        shl160(ca, 8);
+        ean = key_tab[dA < 0 ? -dA : dA];
+      }
+    }
+  }
+  return ge_p3_to_p2(acc);
+}
+
 // Signed radix-16 digits of x < 2^138 (35 digits, d in [-8, 7]) as nibbles d+8, digit i at
 // nibble i+5 of the 5-word output (so digit 34 is the top nibble of word 4).
 __device__ __forceinline__ void recode16_35(const u32 x[5], u32 out[5]) {
@@ -284,7 +399,7 @@ __device__ __forceinline__ void recode256_18(const u32 x[5], u32 out[5]) {
 __device__ __noinline__ void decompress_pair(ge_p3 out[2], const u32* a, const u32* b, u32 ycanon[2][8],
                                              bool ok[2]) {
   const u32* const w[2] = {a, b};
-  ge_decompress2(out, w, ycanon, ok);
+  ge_decompressN<2>(out, w, ycanon, ok);
 }
 
 // k = SHA-512(R || A || M) mod l over the raw input bytes (one block: 96 bytes + padding)
@@ -345,19 +460,19 @@ __device__ bool verify_full(const u32 mw[8], const u32 aw[8], const u32 sigw[16]
 
 // Half-size equation: [d]e = (d s mod l) B - c A - d R == O  (lattice.h).  Sets `fallback`
 // when the reduction failed; the verdict is then decided by verify_full in k_verify_fallback.
-__device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels* sB,
-                            const ge_niels* sB2, const LaneTable& ta, const LaneTable& tr, bool& fallback) {
-  Prologue p;
-  prologue(p, mw, aw, sigw, strict);
-  const lat::HalfScalars h = lat::reduce(p.kw);
-  fallback = !h.ok;
-  // eB = d * s mod l
+__device__ __noinline__ void decompress_one(ge_p3 out[1], const u32* a, u32 ycanon[1][8], bool ok[1]) {
+  const u32* const w[1] = {a};
+  ge_decompressN<1>(out, w, ycanon, ok);
+}
+
+// e_B = d * s mod l, split at 2^140 into radix-256 digit strings (el, eh)
+__device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], u32 el[5], u32 eh[5]) {
   u32 prod[16];
   _Pragma("unroll") for (int i = 0; i < 16; ++i) prod[i] = 0;
   _Pragma("unroll") for (int x = 0; x < 5; ++x) {
     u64 carry = 0;
     _Pragma("unroll") for (int y = 0; y < 8; ++y) {
-      const u64 tt = (u64)h.d[x] * p.sw[y] + prod[x + y] + carry;
+      const u64 tt = (u64)d[x] * s[y] + prod[x + y] + carry;
       prod[x + y] = (u32)tt;
       carry = tt >> 32;
     }
@@ -371,11 +486,51 @@ __device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16]
   _Pragma("unroll") for (int i = 0; i < 4; ++i)
     hi[i] = (eb[4 + i] >> (BASE_SPLIT_BITS - 128)) | (i + 5 < 8 ? eb[5 + i] << (32 - (BASE_SPLIT_BITS - 128)) : 0u);
   hi[4] = 0;
-  u32 cd[5], dd[5], el[5], eh[5];
-  recode16_35(h.c, cd);
-  recode16_35(h.d, dd);
   recode256_18(lo, el);
   recode256_18(hi, eh);
+}
+
+// Half-size equation: [d]e = (d s mod l) B - c A - d R == O  (lattice.h).  Sets `fallback`
+// when the reduction failed; the verdict is then decided by verify_full in k_verify_fallback.
+// When every lane of the wave has its key in the committee cache (wave-uniform test), A comes
+// from the cache: no decompression of A, no per-equation A table, 18 Niels adds for the A term.
+template <bool CACHE>
+__device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels* sB,
+                            const ge_niels* sB2, const LaneTable& ta, const LaneTable& tr, const Committee& cm,
+                            bool& fallback) {
+  const int key = CACHE ? committee_lookup(cm, aw) : -1;
+  if (CACHE && __all(key >= 0)) {
+    u32 rw[8], sw[8];
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) { rw[i] = sigw[i]; sw[i] = sigw[8 + i]; }
+    const bool s_ok = sc_lt_l(sw);
+    ge_p3 R[1];
+    u32 yr[1][8];
+    bool r_ok[1];
+    decompress_one(R, rw, yr, r_ok);
+    const u32 fl = cm.flags[key];
+    const bool small = strict && (((fl >> 1) & 1) || ycanon_is_small_order(yr[0]));
+    const bool ok = s_ok && (fl & 1) && r_ok[0] && !small;
+    u32 kw[8];
+    challenge(rw, aw, mw, kw);
+    const lat::HalfScalars h = lat::reduce(kw);
+    fallback = !h.ok;
+    u32 el[5], eh[5], dd[5], ca[5];
+    base_digits(h.d, sw, el, eh);
+    recode16_35(h.d, dd);
+    recode256_18(h.c, ca);
+    build_table(tr, ge_p3_neg(R[0]));
+    const ge_p2 q = half_scalarmult_cached(tr, dd, ca, h.c_neg, cm.tables + (size_t)key * 129, el, eh, sB, sB2);
+    const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
+    return ok && ident && h.ok;
+  }
+  Prologue p;
+  prologue(p, mw, aw, sigw, strict);
+  const lat::HalfScalars h = lat::reduce(p.kw);
+  fallback = !h.ok;
+  u32 cd[5], dd[5], el[5], eh[5];
+  base_digits(h.d, p.sw, el, eh);
+  recode16_35(h.c, cd);
+  recode16_35(h.d, dd);
   // -c A = |c| * (c < 0 ? A : -A);  -d R = d * (-R)
   build_table(ta, h.c_neg ? p.A : ge_p3_neg(p.A));
   build_table(tr, ge_p3_neg(p.R));
@@ -405,6 +560,7 @@ struct VerifyArgs {
   uint32_t* fb_list;
   uint32_t* fb_count;
   uint32_t force_fb_every;      // test hook: route equations i % every == 0 to the fallback (0 = off)
+  Committee committee;          // n == 0: no cache
 };
 
 __device__ __forceinline__ void load_inputs(const VerifyArgs& a, uint64_t i, u32 mw[8], u32 aw[8], u32 sgw[16]) {
@@ -424,7 +580,7 @@ __device__ __forceinline__ void stage_base_tables(const ge_niels* src, ge_niels*
 #ifndef NWC_VERIFY_WAVES_PER_SIMD
 #define NWC_VERIFY_WAVES_PER_SIMD 2
 #endif
-template <bool HALF>
+template <bool HALF, bool CACHE>
 __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(VerifyArgs a) {
   __shared__ ge_niels sB[HALF ? 2 * 129 : 129];
   stage_base_tables(a.base_table, sB, HALF ? 2 * 129 : 129);
@@ -440,7 +596,7 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
     load_inputs(a, active ? i : 0, mw, aw, sgw);
     bool fb = false;
     bool v;
-    if constexpr (HALF) v = verify_half(mw, aw, sgw, a.strict != 0, sB, sB + 129, ta, tr, fb);
+    if constexpr (HALF) v = verify_half<CACHE>(mw, aw, sgw, a.strict != 0, sB, sB + 129, ta, tr, a.committee, fb);
     else v = verify_full(mw, aw, sgw, a.strict != 0, sB, ta);
     if (HALF && a.force_fb_every && (i % a.force_fb_every) == 0) { fb = true; v = false; }
     v = v && active;
@@ -451,8 +607,9 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
   }
 }
 
-template __global__ void k_verify<true>(VerifyArgs);
-template __global__ void k_verify<false>(VerifyArgs);
+template __global__ void k_verify<true, false>(VerifyArgs);
+template __global__ void k_verify<true, true>(VerifyArgs);
+template __global__ void k_verify<false, false>(VerifyArgs);
 
 // Full-length re-verification of the lanes k_verify could not reduce (rare); sets their bits.
 __global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {

@@ -59,6 +59,12 @@ struct DevCtx {
   uint32_t* fb_count = nullptr;
   size_t fb_cap = 0;
   hipEvent_t scratch_free = nullptr;
+  // committee key cache (nwc_set_committee); buffers replaced only after scratch_free
+  nwc::u32* cm_keys = nullptr;
+  nwc::u32* cm_flags = nullptr;
+  nwc::ge_niels* cm_tables = nullptr;
+  int32_t* cm_slots = nullptr;
+  uint32_t cm_n = 0, cm_slot_mask = 0;
   uint8_t* arena = nullptr;
   size_t arena_cap = 0;
   std::mutex mu;
@@ -95,7 +101,7 @@ int init_device(DevCtx& d) {
   HIP_TRY(hipEventCreateWithFlags(&d.scratch_free, hipEventDisableTiming));
   d.cus = prop.multiProcessorCount;
   int bpc = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify<true>), 256, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify<true, false>), 256, 0));
   d.verify_blocks_per_cu = bpc > 0 ? bpc : 1;
   HIP_TRY(hipMalloc(&d.base_table, 2 * 129 * sizeof(nwc::ge_niels)));
   HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
@@ -159,12 +165,14 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     const char* e = std::getenv("NWC_FORCE_FALLBACK_EVERY");
     return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
   }();
+  const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_slots, d.cm_slot_mask, d.cm_n};
   nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.scratch,
-                    d.fb_list, d.fb_count, force_every};
+                    d.fb_list, d.fb_count, force_every, cm};
   const bool half = half_path();
   if (half) HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
-  if (half) hipLaunchKernelGGL(nwc::k_verify<true>, dim3(grid), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(nwc::k_verify<false>, dim3(grid), dim3(256), 0, s, a);
+  if (half && cm.n) hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a);
+  else if (half) hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((nwc::k_verify<false, false>), dim3(grid), dim3(256), 0, s, a);
   HIP_TRY(hipGetLastError());
   if (half) {
     const unsigned fgrid = grid < (unsigned)d.cus ? grid : (unsigned)d.cus;
@@ -306,6 +314,10 @@ void nwc_shutdown(void) {
     if (d->scratch) (void)hipFree(d->scratch);
     if (d->fb_list) (void)hipFree(d->fb_list);
     if (d->fb_count) (void)hipFree(d->fb_count);
+    if (d->cm_keys) (void)hipFree(d->cm_keys);
+    if (d->cm_flags) (void)hipFree(d->cm_flags);
+    if (d->cm_tables) (void)hipFree(d->cm_tables);
+    if (d->cm_slots) (void)hipFree(d->cm_slots);
     if (d->scratch_free) (void)hipEventDestroy(d->scratch_free);
     if (d->base_table) (void)hipFree(d->base_table);
     if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -408,7 +420,57 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
 int nwc_set_committee(const uint8_t* pks, size_t n) {
   if (int rc = require_init()) return rc;
   if (n && !pks) return set_err(NWC_ERR_ARG, "null buffer");
-  return 0;  // verdicts never depend on the cache; keys are decoded per equation in this version
+  if (n > (1u << 20)) return set_err(NWC_ERR_ARG, "committee of %zu keys is too large", n);
+  // open-addressing table (exact 32-byte keys), load factor <= 1/4, probe length bounded
+  std::vector<nwc::u32> keys(8 * n);
+  std::memcpy(keys.data(), pks, 32 * n);
+  uint32_t slots = 16;
+  while (slots < 4 * n) slots <<= 1;
+  std::vector<int32_t> table;
+  for (;;) {
+    table.assign(slots, -1);
+    bool fits = true;
+    for (size_t i = 0; i < n && fits; ++i) {
+      const nwc::u32 h = nwc::committee_hash(keys[8 * i], keys[8 * i + 1]);
+      int p = 0;
+      for (; p < nwc::COMMITTEE_MAX_PROBE; ++p) {
+        int32_t& slot = table[(h + p) & (slots - 1)];
+        if (slot < 0) { slot = (int32_t)i; break; }
+        if (std::memcmp(&keys[8 * slot], &keys[8 * i], 32) == 0) break;   // duplicate key
+      }
+      fits = p < nwc::COMMITTEE_MAX_PROBE;
+    }
+    if (fits) break;
+    slots <<= 1;
+  }
+  for (auto& dp : g_devs) {
+    DevCtx& d = *dp;
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipEventSynchronize(d.scratch_free));   // no verify launch still reads the old cache
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    if (d.cm_keys) HIP_TRY(hipFree(d.cm_keys));
+    if (d.cm_flags) HIP_TRY(hipFree(d.cm_flags));
+    if (d.cm_tables) HIP_TRY(hipFree(d.cm_tables));
+    if (d.cm_slots) HIP_TRY(hipFree(d.cm_slots));
+    d.cm_keys = nullptr; d.cm_flags = nullptr; d.cm_tables = nullptr; d.cm_slots = nullptr;
+    d.cm_n = 0; d.cm_slot_mask = 0;
+    if (n == 0) continue;
+    HIP_TRY(hipMalloc(&d.cm_keys, 32 * n));
+    HIP_TRY(hipMalloc(&d.cm_flags, 4 * n));
+    HIP_TRY(hipMalloc(&d.cm_tables, n * 129 * sizeof(nwc::ge_niels)));
+    HIP_TRY(hipMalloc(&d.cm_slots, 4 * (size_t)slots));
+    HIP_TRY(hipMemcpyAsync(d.cm_keys, keys.data(), 32 * n, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.cm_slots, table.data(), 4 * (size_t)slots, hipMemcpyHostToDevice, d.stream));
+    const unsigned grid = (unsigned)((n * 129 + 255) / 256);
+    hipLaunchKernelGGL(nwc::k_build_key_tables, dim3(grid), dim3(256), 0, d.stream, d.cm_keys, (nwc::u32)n,
+                       d.cm_tables, d.cm_flags);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    d.cm_n = (uint32_t)n;
+    d.cm_slot_mask = slots - 1;
+  }
+  return 0;
 }
 
 int nwc_sha512_trunc32_many(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32) {
