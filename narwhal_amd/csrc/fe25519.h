@@ -76,62 +76,35 @@ FE_DEV fe fe_carry_wide(i64 h[10]) {
   return out;
 }
 
+}  // namespace nwc
+#include "fe_asm.h"
+namespace nwc {
+
 // h = f * g.  Column k collects f_i g_j for i + j = k (mod 10); a wrapped term (i + j >= 10)
 // carries the factor 19 (2^255 = 19 mod p), and a term with both i, j odd carries 2
 // (26 + 25 offsets).  The 19 goes on g (|19 g_j| < 2^31), the 2 on f (|2 f_i| < 2^27).
+// The products are one asm block (fe_asm.h, tools/gen_fe_asm.py): per column one
+// v_mad_i64_i32 chain seeded with the rounding bias, columns interleaved.
 FE_DEV fe fe_mul(const fe& f, const fe& g) {
-  i32 g19[10], f2[10];
-  _Pragma("unroll") for (int i = 0; i < 10; ++i) { g19[i] = (i32)(19u * (u32)g.v[i]); f2[i] = (i32)(2u * (u32)f.v[i]); }
   i64 h[10];
-  _Pragma("unroll") for (int k = 0; k < 10; ++k) {
-    i64 acc = fe_col_bias(k);
-    _Pragma("unroll") for (int i = 0; i < 10; ++i) {
-      const int j = (k - i + 10) % 10;
-      const bool wrap = (i + j) >= 10;
-      const i32 fi = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-      const i32 gj = wrap ? g19[j] : g.v[j];
-      acc += (i64)fi * (i64)gj;
-    }
-    h[k] = acc;
-  }
+  fe_mul_wide_asm(f, g, h);
   return fe_carry_wide(h);
 }
 
 // h = f^2: 55 distinct products.  Off-diagonal terms carry 2 (symmetry) on the left factor;
 // the odd-odd 2 and the wrap 19 go on the right factor (|38 f_j| < 2^31 for odd j).
-FE_DEV void fe_sq_wide(const fe& f, i64 h[10]) {
-  i32 f2[10], f19[10], f38[10];
-  _Pragma("unroll") for (int i = 0; i < 10; ++i) {
-    f2[i] = (i32)(2u * (u32)f.v[i]); f19[i] = (i32)(19u * (u32)f.v[i]); f38[i] = (i32)(38u * (u32)f.v[i]);
-  }
-  _Pragma("unroll") for (int k = 0; k < 10; ++k) {
-    i64 acc = 0;   // fe_sq / fe_sq2 add the column bias after (fe_sq2 doubles first)
-    _Pragma("unroll") for (int i = 0; i < 10; ++i) {
-      _Pragma("unroll") for (int j = i; j < 10; ++j) {
-        if ((i + j) % 10 != k) continue;
-        const bool wrap = (i + j) >= 10;
-        const bool oo = (i & 1) && (j & 1);
-        i32 left = (i == j) ? f.v[i] : f2[i];
-        i32 right;
-        if (wrap) right = oo ? f38[j] : f19[j];
-        else right = oo ? f2[j] : f.v[j];
-        acc += (i64)left * (i64)right;
-      }
-    }
-    h[k] = acc;
-  }
-}
 FE_DEV fe fe_sq(const fe& f) {
-  i64 h[10]; fe_sq_wide(f, h);
-  _Pragma("unroll") for (int i = 0; i < 10; ++i) h[i] += fe_col_bias(i);
+  i64 h[10];
+  fe_sq_wide_asm(f, h);
   return fe_carry_wide(h);
 }
 
 // 2 f^2, doubled before the carry so the result is tight (the 2Z^2 term of point doubling
-// is then combined with two more tight terms and stays within the loose bound).
+// is then combined with two more tight terms and stays within the loose bound).  The 2 goes on
+// the left factors (|4 f_i| < 2^29).
 FE_DEV fe fe_sq2(const fe& f) {
-  i64 h[10]; fe_sq_wide(f, h);
-  _Pragma("unroll") for (int i = 0; i < 10; ++i) h[i] = h[i] + h[i] + fe_col_bias(i);
+  i64 h[10];
+  fe_sq2_wide_asm(f, h);
   return fe_carry_wide(h);
 }
 

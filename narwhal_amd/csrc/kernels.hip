@@ -89,8 +89,8 @@ __device__ void sha512_one_block(const u32* words, int len, u32 digest_le[16]) {
 }
 
 // ------------------------------------------------------------------------------- base tables
-// table[i] = i*B and table[129 + i] = i*(2^140 B), i = 0..128, affine Niels.  One lane per entry.
-constexpr int BASE_SPLIT_BITS = 140;
+// table[i] = i*B and table[129 + i] = i*(2^132 B), i = 0..128, affine Niels.  One lane per entry.
+constexpr int BASE_SPLIT_BITS = 132;
 __global__ void k_build_base_table(ge_niels* table) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * 129) return;
@@ -244,40 +244,117 @@ __device__ __forceinline__ ge_p2 double_scalarmult(const LaneTable& tab, u32 kd[
   return ge_p1p1_to_p2(t);
 }
 
-// ---- half-size ladder: Q = eB*B + c'*PA + d*PR over 35 radix-16 windows (140 bits) -----------
-// cd/dd: radix-16 digits (nibble d+8) of |c| and d, digit 34 at the top of word 4;
-// el/eh: radix-256 digits (byte d+128) of eB mod 2^140 and eB >> 140, digit 17 at the top.
-constexpr int HALF_WINDOWS = 35;
-__device__ __forceinline__ void shl160(u32 d[5], int bits) {
-  _Pragma("unroll") for (int i = 4; i > 0; --i) d[i] = (d[i] << bits) | (d[i - 1] >> (32 - bits));
-  d[0] <<= bits;
+// ---- half-size ladder: Q = eB*B + c'*PA + d*PR over W radix-16 windows -----------------------
+// W is wave-uniform: the smallest W in [33, 37] with |c|, d < 2^(4W-1) for every lane of the
+// wave (max(|c|, d) has 127-128 bits typically; ~9 % of waves hold a lane of 132+ bits and run
+// 34-35 windows, and only |c| or d >= 2^147 -- never seen in 10^6 samples -- leaves the
+// half-size path).  The basepoint scalar eB = d s mod l is split at 2^132 into two 17-digit
+// radix-256 strings added at the even windows w <= 32.
+// Digit streams are packed so the next digit is always in the top nibble/byte of word 4 and is
+// consumed by shifting the 160-bit string left:
+//   Digits16  {w[5], top}: signed radix-16 digits of x < 2^(4W-1): digits 0..W-2 in [-8, 7] as
+//     nibbles d+8 (digit W-2 in the top nibble), digit W-1 = top in [0, 8].
+//   Digits256 {w[5]}: signed radix-256 digits as bytes d+128, the first digit to use in the top byte.
+// The accumulator between operations is kept in completed (p1p1) form `t`: an add converts it to
+// extended (4M) because the addition needs T; a doubling only needs (X:Y:Z) (3M).  So the last
+// add of each window feeds the next window's doublings at 3M instead of 4M.
+constexpr int HALF_WINDOWS_MIN = 33, HALF_WINDOWS_MAX = 37;
+constexpr int B_DIGITS = 17;   // radix-256 digits of each half of eB (windows 32, 30, ..., 0)
+struct Digits16 { u32 w[5]; i32 top; };
+struct Digits256 { u32 w[5]; };
+
+__device__ __forceinline__ i32 next16(Digits16& x) {
+  const i32 d = (i32)(x.w[4] >> 28) - 8;
+  _Pragma("unroll") for (int i = 4; i > 0; --i) x.w[i] = (x.w[i] << 4) | (x.w[i - 1] >> 28);
+  x.w[0] <<= 4;
+  return d;
+}
+__device__ __forceinline__ i32 next256(Digits256& x) {
+  const i32 d = (i32)(x.w[4] >> 24) - 128;
+  _Pragma("unroll") for (int i = 4; i > 0; --i) x.w[i] = (x.w[i] << 8) | (x.w[i - 1] >> 24);
+  x.w[0] <<= 8;
+  return d;
+}
+// 160-bit left shift by a wave-uniform bit count s in [0, 32]
+__device__ __forceinline__ void shl160_dyn(u32 w[5], u32 s) {
+  if (s == 32) {
+    _Pragma("unroll") for (int i = 4; i > 0; --i) w[i] = w[i - 1];
+    w[0] = 0;
+  } else if (s) {
+    _Pragma("unroll") for (int i = 4; i > 0; --i) w[i] = (w[i] << s) | (w[i - 1] >> (32 - s));
+    w[0] <<= s;
+  }
 }
 
-__device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const LaneTable& tr, u32 cd[5], u32 dd[5],
-                                                 u32 el[5], u32 eh[5], const ge_niels* sB, const ge_niels* sB2) {
+// Signed radix-16 digits of x < 2^(4W-1) for a wave-uniform W in [33, 37].
+__device__ __forceinline__ Digits16 recode16(const u32 x[5], int W) {
+  Digits16 r;
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) r.w[i] = 0;
+  r.top = 0;
+  i32 carry = 0;
+  _Pragma("unroll") for (int i = 0; i < HALF_WINDOWS_MAX - 1; ++i) {
+    const i32 v = (i32)((x[i >> 3] >> (4 * (i & 7))) & 15u) + carry;
+    if (i == W - 1) r.top = v;
+    carry = (v + 8) >> 4;
+    const i32 d = v - (carry << 4);
+    const int pos = i + 4;   // digit 35 in the top nibble of word 4
+    r.w[pos >> 3] |= (u32)(d + 8) << (4 * (pos & 7));
+  }
+  if (W == HALF_WINDOWS_MAX) r.top = (i32)((x[4] >> 16) & 15u) + carry;
+  // move digit W-2 to the top nibble (digits >= W-1 leave the string)
+  shl160_dyn(r.w, 4u * (u32)(HALF_WINDOWS_MAX - W));
+  return r;
+}
+// Signed radix-256 digits of x < 2^(8 ndig - 1) (ndig <= 19, d in [-128, 128]) as bytes d+128
+// with digit ndig-1 in the top byte of word 4.  ndig may be wave-uniform dynamic.
+__device__ __forceinline__ Digits256 recode256(const u32 x[5], int ndig) {
+  Digits256 r;
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) r.w[i] = 0;
+  i32 carry = 0;
+  _Pragma("unroll") for (int i = 0; i < 19; ++i) {
+    i32 d = (i32)((x[i >> 2] >> (8 * (i & 3))) & 255u) + carry;
+    carry = (d + 128) >> 8;
+    d -= carry << 8;
+    const int pos = i + 1;   // digit 18 in the top byte of word 4
+    r.w[pos >> 2] |= (u32)(d + 128) << (8 * (pos & 3));
+  }
+  shl160_dyn(r.w, 8u * (u32)(19 - ndig));
+  return r;
+}
+
+// Smallest W in [33, 37] with x < 2^(4W-1) for all lanes (bits = bit length per lane); 38 if none.
+__device__ __forceinline__ int wave_windows(int bits) {
+  int W = HALF_WINDOWS_MIN;
+  _Pragma("unroll") for (int k = HALF_WINDOWS_MIN; k <= HALF_WINDOWS_MAX; ++k)
+    W += __any(bits > 4 * k - 1) ? 1 : 0;
+  return W;
+}
+
+__device__ __forceinline__ ge_p1p1 ge_p1p1_identity() {
+  ge_p1p1 r; r.X = fe_zero(); r.Y = fe_one(); r.Z = fe_one(); r.T = fe_one(); return r;
+}
+
+// four doublings of t (t in, t out), (X:Y:Z) only
+__device__ __forceinline__ void ladder_dbl4(ge_p1p1& t) {
+  ge_p2 p2 = ge_p1p1_to_p2(t);
+#pragma unroll 1
+  for (int j = 0; j < 3; ++j) { t = ge_p2_dbl(p2); p2 = ge_p1p1_to_p2(t); }
+  t = ge_p2_dbl(p2);
+}
+
+__device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const LaneTable& tr, Digits16 cd, Digits16 dd,
+                                                 Digits256 el, Digits256 eh, const ge_niels* sB, const ge_niels* sB2,
+                                                 int W) {
   // Code-size discipline: the window body holds ONE doubling, ONE cached add and ONE Niels add
-  // (each in a rolled loop) so the hot loop (~30 KB) stays inside the instruction cache; fully
-  // inlined it was ~77 KB.  Each add leaves the accumulator in extended form; the next window's
-  // doublings start from its (X:Y:Z).
-  ge_p3 acc = ge_p3_identity();
+  // (each in a rolled loop) so the hot loop stays inside the instruction cache.
+  ge_p1p1 t = ge_p1p1_identity();
   // Entries for the current window are loaded at the end of the previous window, so their
   // latency hides behind this window's doublings and only 80 registers are in flight.
-  i32 da = (i32)(cd[4] >> 28) - 8;
-  i32 dr = (i32)(dd[4] >> 28) - 8;
-  shl160(cd, 4);
-  shl160(dd, 4);
-  ge_cached ea = ta.load(da < 0 ? -da : da);
-  ge_cached er = tr.load(dr < 0 ? -dr : dr);
+  i32 da = cd.top, dr = dd.top;
+  ge_cached ea = ta.load(da), er = tr.load(dr);
 #pragma unroll 1
-  for (int w = HALF_WINDOWS - 1; w >= 0; --w) {
-    if (w != HALF_WINDOWS - 1) {
-      ge_p2 p2 = ge_p3_to_p2(acc);
-      ge_p1p1 t;
-#pragma unroll 1
-      for (int j = 0; j < 3; ++j) { t = ge_p2_dbl(p2); p2 = ge_p1p1_to_p2(t); }
-      t = ge_p2_dbl(p2);
-      acc = ge_p1p1_to_p3(t);
-    }
+  for (int w = W - 1; w >= 0; --w) {
+    if (w != W - 1) ladder_dbl4(t);
 #pragma unroll 1
     for (int side = 0; side < 2; ++side) {
       const bool neg = side ? (dr < 0) : (da < 0);
@@ -286,68 +363,52 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
       q.YmX = fe_select(ea.YmX, er.YmX, side != 0);
       q.Z = fe_select(ea.Z, er.Z, side != 0);
       q.T2d = fe_select(ea.T2d, er.T2d, side != 0);
-      acc = ge_p1p1_to_p3(ge_add_cached(acc, ge_cached_cneg(q, neg)));
+      t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(q, neg));
     }
     if (w > 0) {
-      da = (i32)(cd[4] >> 28) - 8;
-      dr = (i32)(dd[4] >> 28) - 8;
-      shl160(cd, 4);
-      shl160(dd, 4);
+      da = next16(cd);
+      dr = next16(dd);
       ea = ta.load(da < 0 ? -da : da);
       er = tr.load(dr < 0 ? -dr : dr);
     }
-    if ((w & 1) == 0) {
-      const i32 d0 = (i32)(el[4] >> 24) - 128;
-      const i32 d1 = (i32)(eh[4] >> 24) - 128;
-      shl160(el, 8);
-      shl160(eh, 8);
+    if ((w & 1) == 0 && w < 2 * B_DIGITS) {
+      const i32 d0 = next256(el), d1 = next256(eh);
 #pragma unroll 1
       for (int side = 0; side < 2; ++side) {
         const i32 dd_ = side ? d1 : d0;
         const ge_niels nb = (side ? sB2 : sB)[dd_ < 0 ? -dd_ : dd_];
-        acc = ge_p1p1_to_p3(ge_add_niels(acc, ge_niels_cneg(nb, dd_ < 0)));
+        t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(nb, dd_ < 0));
       }
     }
   }
-  return ge_p3_to_p2(acc);
+  return ge_p1p1_to_p2(t);
 }
 
 // Half-size ladder with a cached key: Q = eB*B + c'*(-A) + d*(-R) where the A term uses the key's
-// radix-256 Niels table (18 adds at even windows, no per-equation table or decompression).
-// ca: radix-256 digits of |c| (byte d+128, digit 17 at the top); c_neg flips every A entry.
-__device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, u32 dd[5], u32 ca[5], bool c_neg,
-                                                        const ge_niels* key_tab, u32 el[5], u32 eh[5],
-                                                        const ge_niels* sB, const ge_niels* sB2) {
-  ge_p3 acc = ge_p3_identity();
-  i32 dr = (i32)(dd[4] >> 28) - 8;
-  shl160(dd, 4);
-  ge_cached er = tr.load(dr < 0 ? -dr : dr);
-  i32 dA = (i32)(ca[4] >> 24) - 128;
-  shl160(ca, 8);
+// radix-256 Niels table (one add at every even window, no per-equation table or decompression).
+// ca: radix-256 digits of |c| starting at window (W-1) & ~1; c_neg flips every A entry.
+__device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Digits16 dd, Digits256 ca, bool c_neg,
+                                                        const ge_niels* key_tab, Digits256 el, Digits256 eh,
+                                                        const ge_niels* sB, const ge_niels* sB2, int W) {
+  ge_p1p1 t = ge_p1p1_identity();
+  i32 dr = dd.top;
+  ge_cached er = tr.load(dr);
+  i32 dA = next256(ca);
   ge_niels ean = key_tab[dA < 0 ? -dA : dA];
 #pragma unroll 1
-  for (int w = HALF_WINDOWS - 1; w >= 0; --w) {
-    if (w != HALF_WINDOWS - 1) {
-      ge_p2 p2 = ge_p3_to_p2(acc);
-      ge_p1p1 t;
-#pragma unroll 1
-      for (int j = 0; j < 3; ++j) { t = ge_p2_dbl(p2); p2 = ge_p1p1_to_p2(t); }
-      t = ge_p2_dbl(p2);
-      acc = ge_p1p1_to_p3(t);
-    }
-    acc = ge_p1p1_to_p3(ge_add_cached(acc, ge_cached_cneg(er, dr < 0)));
+  for (int w = W - 1; w >= 0; --w) {
+    if (w != W - 1) ladder_dbl4(t);
+    t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
     if (w > 0) {
-      dr = (i32)(dd[4] >> 28) - 8;
-      shl160(dd, 4);
+      dr = next16(dd);
       er = tr.load(dr < 0 ? -dr : dr);
     }
     if ((w & 1) == 0) {
-      const i32 d0 = (i32)(el[4] >> 24) - 128;
-      const i32 d1 = (i32)(eh[4] >> 24) - 128;
-      shl160(el, 8);
-      shl160(eh, 8);
+      const bool with_b = w < 2 * B_DIGITS;
+      const i32 d0 = with_b ? next256(el) : 0, d1 = with_b ? next256(eh) : 0;
+      const int sides = with_b ? 3 : 1;
 #pragma unroll 1
-      for (int side = 0; side < 3; ++side) {
+      for (int side = 0; side < sides; ++side) {
         ge_niels nb;
         bool neg;
         if (side == 0) {
@@ -358,48 +419,24 @@ __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, u32
           nb = (side == 1 ? sB : sB2)[dd_ < 0 ? -dd_ : dd_];
           neg = dd_ < 0;
         }
-        acc = ge_p1p1_to_p3(ge_add_niels(acc, ge_niels_cneg(nb, neg)));
+        t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(nb, neg));
       }
       if (w > 0) {
-        dA = (i32)(ca[4] >> 24) - 128;
-        shl160(ca, 8);
+        dA = next256(ca);
         ean = key_tab[dA < 0 ? -dA : dA];
       }
     }
   }
-  return ge_p3_to_p2(acc);
+  return ge_p1p1_to_p2(t);
 }
 
-// Signed radix-16 digits of x < 2^138 (35 digits, d in [-8, 7]) as nibbles d+8, digit i at
-// nibble i+5 of the 5-word output (so digit 34 is the top nibble of word 4).
-__device__ __forceinline__ void recode16_35(const u32 x[5], u32 out[5]) {
-  _Pragma("unroll") for (int i = 0; i < 5; ++i) out[i] = 0;
-  i32 carry = 0;
-  _Pragma("unroll") for (int i = 0; i < HALF_WINDOWS; ++i) {
-    i32 d = (i32)((x[i >> 3] >> (4 * (i & 7))) & 15u) + carry;
-    carry = (d + 8) >> 4;
-    d -= carry << 4;
-    const int pos = i + 5;
-    out[pos >> 3] |= (u32)(d + 8) << (4 * (pos & 7));
-  }
-}
-// Signed radix-256 digits of x < 2^140 (18 digits) as bytes d+128, digit i at byte i+2.
-__device__ __forceinline__ void recode256_18(const u32 x[5], u32 out[5]) {
-  _Pragma("unroll") for (int i = 0; i < 5; ++i) out[i] = 0;
-  i32 carry = 0;
-  _Pragma("unroll") for (int i = 0; i < 18; ++i) {
-    i32 d = (i32)((x[i >> 2] >> (8 * (i & 3))) & 255u) + carry;
-    carry = (d + 128) >> 8;
-    d -= carry << 8;
-    const int pos = i + 2;
-    out[pos >> 2] |= (u32)(d + 128) << (8 * (pos & 3));
-  }
-}
-
-__device__ __noinline__ void decompress_pair(ge_p3 out[2], const u32* a, const u32* b, u32 ycanon[2][8],
-                                             bool ok[2]) {
-  const u32* const w[2] = {a, b};
-  ge_decompressN<2>(out, w, ycanon, ok);
+// One decompression per call (a noinline body shared by every call site: I-cache).  The two
+// points of an equation are decoded one after the other; each field op inside is already 10
+// independent multiply-accumulate chains (fe_asm.h), and interleaving two exponentiations
+// doubled the live field elements past the 2-waves/SIMD register budget.
+__device__ __noinline__ void decompress_one(ge_p3 out[1], const u32* a, u32 ycanon[1][8], bool ok[1]) {
+  const u32* const w[1] = {a};
+  ge_decompressN<1>(out, w, ycanon, ok);
 }
 
 // k = SHA-512(R || A || M) mod l over the raw input bytes (one block: 96 bytes + padding)
@@ -433,14 +470,12 @@ __device__ __forceinline__ void prologue(Prologue& p, const u32 mw[8], const u32
   u32 rw[8];
   _Pragma("unroll") for (int i = 0; i < 8; ++i) { rw[i] = sigw[i]; p.sw[i] = sigw[8 + i]; }
   const bool s_ok = sc_lt_l(p.sw);
-  ge_p3 AR[2];
-  u32 ycan[2][8];
-  bool okp[2];
-  decompress_pair(AR, aw, rw, ycan, okp);
-  p.A = AR[0];
-  p.R = AR[1];
-  const bool small = strict && (ycanon_is_small_order(ycan[0]) || ycanon_is_small_order(ycan[1]));
-  p.ok = s_ok && okp[0] && okp[1] && !small;
+  u32 ya[1][8], yr[1][8];
+  bool oka[1], okr[1];
+  decompress_one(&p.A, aw, ya, oka);
+  decompress_one(&p.R, rw, yr, okr);
+  const bool small = strict && (ycanon_is_small_order(ya[0]) || ycanon_is_small_order(yr[0]));
+  p.ok = s_ok && oka[0] && okr[0] && !small;
   challenge(rw, aw, mw, p.kw);
 }
 
@@ -458,15 +493,8 @@ __device__ bool verify_full(const u32 mw[8], const u32 aw[8], const u32 sigw[16]
   return p.ok && eq;
 }
 
-// Half-size equation: [d]e = (d s mod l) B - c A - d R == O  (lattice.h).  Sets `fallback`
-// when the reduction failed; the verdict is then decided by verify_full in k_verify_fallback.
-__device__ __noinline__ void decompress_one(ge_p3 out[1], const u32* a, u32 ycanon[1][8], bool ok[1]) {
-  const u32* const w[1] = {a};
-  ge_decompressN<1>(out, w, ycanon, ok);
-}
-
-// e_B = d * s mod l, split at 2^140 into radix-256 digit strings (el, eh)
-__device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], u32 el[5], u32 eh[5]) {
+// e_B = d * s mod l, split at 2^132 into radix-256 digit strings (el, eh)
+__device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digits256& el, Digits256& eh) {
   u32 prod[16];
   _Pragma("unroll") for (int i = 0; i < 16; ++i) prod[i] = 0;
   _Pragma("unroll") for (int x = 0; x < 5; ++x) {
@@ -480,14 +508,14 @@ __device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], u32 
   }
   u32 eb[8];
   sc_reduce512(prod, eb);
+  constexpr int SH = BASE_SPLIT_BITS - 128;
   u32 lo[5], hi[5];
   _Pragma("unroll") for (int i = 0; i < 4; ++i) lo[i] = eb[i];
-  lo[4] = eb[4] & ((1u << (BASE_SPLIT_BITS - 128)) - 1u);
-  _Pragma("unroll") for (int i = 0; i < 4; ++i)
-    hi[i] = (eb[4 + i] >> (BASE_SPLIT_BITS - 128)) | (i + 5 < 8 ? eb[5 + i] << (32 - (BASE_SPLIT_BITS - 128)) : 0u);
+  lo[4] = eb[4] & ((1u << SH) - 1u);
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) hi[i] = (eb[4 + i] >> SH) | (i + 5 < 8 ? eb[5 + i] << (32 - SH) : 0u);
   hi[4] = 0;
-  recode256_18(lo, el);
-  recode256_18(hi, eh);
+  el = recode256(lo, B_DIGITS);
+  eh = recode256(hi, B_DIGITS);
 }
 
 // Half-size equation: [d]e = (d s mod l) B - c A - d R == O  (lattice.h).  Sets `fallback`
@@ -513,28 +541,30 @@ __device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16]
     u32 kw[8];
     challenge(rw, aw, mw, kw);
     const lat::HalfScalars h = lat::reduce(kw);
+    // odd W: the top radix-256 digit of |c| (window W-1) is then < 2^3 + 1, never 128
+    const int W = wave_windows(h.ok ? h.bits : 0) | 1;
     fallback = !h.ok;
-    u32 el[5], eh[5], dd[5], ca[5];
+    Digits256 el, eh;
     base_digits(h.d, sw, el, eh);
-    recode16_35(h.d, dd);
-    recode256_18(h.c, ca);
+    const Digits16 dd = recode16(h.d, W);
+    const Digits256 ca = recode256(h.c, ((W - 1) >> 1) + 1);
     build_table(tr, ge_p3_neg(R[0]));
-    const ge_p2 q = half_scalarmult_cached(tr, dd, ca, h.c_neg, cm.tables + (size_t)key * 129, el, eh, sB, sB2);
+    const ge_p2 q = half_scalarmult_cached(tr, dd, ca, h.c_neg, cm.tables + (size_t)key * 129, el, eh, sB, sB2, W);
     const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
     return ok && ident && h.ok;
   }
   Prologue p;
   prologue(p, mw, aw, sigw, strict);
   const lat::HalfScalars h = lat::reduce(p.kw);
+  const int W = wave_windows(h.ok ? h.bits : 0);
   fallback = !h.ok;
-  u32 cd[5], dd[5], el[5], eh[5];
+  Digits256 el, eh;
   base_digits(h.d, p.sw, el, eh);
-  recode16_35(h.c, cd);
-  recode16_35(h.d, dd);
+  const Digits16 cd = recode16(h.c, W), dd = recode16(h.d, W);
   // -c A = |c| * (c < 0 ? A : -A);  -d R = d * (-R)
   build_table(ta, h.c_neg ? p.A : ge_p3_neg(p.A));
   build_table(tr, ge_p3_neg(p.R));
-  const ge_p2 q = half_scalarmult(ta, tr, cd, dd, el, eh, sB, sB2);
+  const ge_p2 q = half_scalarmult(ta, tr, cd, dd, el, eh, sB, sB2, W);
   const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
   return p.ok && ident && h.ok;
 }
@@ -653,59 +683,59 @@ __global__ void k_cert_reduce(const uint64_t* __restrict__ leaf_bits, const uint
 
 // ------------------------------------------------------------------------------- SHA-512 digests
 // digest32 of message i = data[offsets[i] .. (ends ? ends[i] : offsets[i+1])).  One lane per
-// message; a 16-byte-aligned start takes the dwordx4 path.
-__global__ __launch_bounds__(256) void k_sha512_digest32(const uint8_t* __restrict__ data,
-                                                         const uint64_t* __restrict__ offsets,
-                                                         const uint64_t* __restrict__ ends,
-                                                         uint64_t n, uint8_t* __restrict__ out32) {
+// message.  One compression site for every block kind (a fully unrolled compression is ~3.3k
+// instructions; three inlined copies would not share the instruction cache): each block's 16
+// words come from 8 dwordx4 loads when the block is whole and the message start is 16-byte
+// aligned, otherwise from byte loads with the FIPS 180-4 padding (0x80, zeros, 128-bit big-endian
+// bit length) built in place.  Lanes of different lengths stay converged on the compression.
+struct ShaBlock { uint64_t w[16]; };
+__device__ __noinline__ ShaBlock sha_block_bytes(const uint8_t* p, uint64_t len, uint64_t b) {
+  // bytes [128 b, 128 b + 128) of the padded message
+  ShaBlock r;
+  uint64_t* w = r.w;
+  const uint64_t base = b << 7;
+  const uint64_t padded_blocks = (len + 17 + 127) >> 7;
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) {
+    uint64_t x = 0;
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) {
+      const uint64_t idx = base + 8 * j + k;
+      const uint32_t byte = idx < len ? p[idx] : (idx == len ? 0x80u : 0u);
+      x = (x << 8) | byte;
+    }
+    w[j] = x;
+  }
+  if (b + 1 == padded_blocks) { w[14] = len >> 61; w[15] = len << 3; }
+  return r;
+}
+
+__global__ __launch_bounds__(256, 2) void k_sha512_digest32(const uint8_t* __restrict__ data,
+                                                            const uint64_t* __restrict__ offsets,
+                                                            const uint64_t* __restrict__ ends,
+                                                            uint64_t n, uint8_t* __restrict__ out32) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t start = offsets[i];
   const uint64_t len = (ends ? ends[i] : offsets[i + 1]) - start;
   const uint8_t* p = data + start;
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint64_t fast = (start & 15) == 0 ? (len >> 7) : 0;   // whole, aligned blocks
+  const uint64_t total = (len + 17 + 127) >> 7;                 // blocks incl. padding
   uint64_t st[8];
   sha512_init_state(st);
-  const uint64_t nfull = len >> 7;
-  uint64_t w[16];
-  if ((start & 15) == 0) {
-    const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll 1
-    for (uint64_t b = 0; b < nfull; ++b) {
+  for (uint64_t b = 0; b < total; ++b) {
+    uint64_t w[16];
+    if (__builtin_expect(b < fast, 1)) {
       uint4 v[8];
       _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] = q[8 * b + j];
       _Pragma("unroll") for (int j = 0; j < 8; ++j) {
         w[2 * j] = be64_from_le32(v[j].x, v[j].y);
         w[2 * j + 1] = be64_from_le32(v[j].z, v[j].w);
       }
-      sha512_compress(st, w);
+    } else {
+      const ShaBlock r = sha_block_bytes(p, len, b);
+      _Pragma("unroll") for (int j = 0; j < 16; ++j) w[j] = r.w[j];
     }
-  } else {
-#pragma unroll 1
-    for (uint64_t b = 0; b < nfull; ++b) {
-      _Pragma("unroll") for (int j = 0; j < 16; ++j) {
-        uint64_t x = 0;
-        _Pragma("unroll") for (int k = 0; k < 8; ++k) x = (x << 8) | p[128 * b + 8 * j + k];
-        w[j] = x;
-      }
-      sha512_compress(st, w);
-    }
-  }
-  // tail: rem bytes + 0x80 + zeros + 128-bit big-endian bit length (1 or 2 blocks)
-  const uint32_t rem = (uint32_t)(len - (nfull << 7));
-  const uint8_t* t = p + (nfull << 7);
-  const int nblk = rem <= 111 ? 1 : 2;
-#pragma unroll 1
-  for (int blk = 0; blk < nblk; ++blk) {
-    _Pragma("unroll") for (int j = 0; j < 16; ++j) {
-      uint64_t x = 0;
-      _Pragma("unroll") for (int k = 0; k < 8; ++k) {
-        const uint32_t idx = (uint32_t)(128 * blk + 8 * j + k);
-        const uint32_t byte = idx < rem ? t[idx] : (idx == rem ? 0x80u : 0u);
-        x = (x << 8) | byte;
-      }
-      w[j] = x;
-    }
-    if (blk == nblk - 1) { w[14] = len >> 61; w[15] = len << 3; }
     sha512_compress(st, w);
   }
   uint32_t* o = reinterpret_cast<uint32_t*>(out32 + 32 * i);

@@ -4,20 +4,21 @@
 // SURVEY.md A.3 step 5, A.5) needs 252 shared doublings for the 253-bit k.  Following the
 // lattice-reduction idea of Pornin ("Optimized lattice basis reduction in dimension 2, and fast
 // Schnorr and EdDSA signature verification", 2020), find (c, d) with
-//       d * k = c  (mod 8l),   d odd,   |c|, |d| < 2^138,
+//       d * k = c  (mod 8l),   d odd,   |c|, |d| < 2^146,
 // then  [d] e = (d s mod l) B - c A - d R.   Because |E| = 8l and d is odd with 0 < d < l,
 // multiplication by d is injective on E (= Z_l x Z_8), so [d] e = O  <=>  e = O: the verdict is
 // exactly dalek's, for every A and R including small/mixed-order ones (the modulus is 8l, not l,
 // so (dk - c) A = O holds for points with torsion too).  The multi-scalar multiplication then
-// needs only ~136 doublings.
+// needs only 128 doublings (33 radix-16 windows) for typical k.
 //
 // (c, d) come from the continued-fraction expansion of k / (8l) (Euclid on r_{-1} = 8l,
 // r_0 = k with cofactors t): stop at the first r_i < 2^127; if t_i is even, take the best odd
 // combination (r_{i-1} - m r_i, t_{i-1} - m t_i).  Quotients are estimated from the top 64 bits
 // in double precision and always under-estimated, so each step subtracts q <= floor(r0/r1)
 // copies and the remainder sequence is exactly Euclid's.  A lane that does not converge within
-// the iteration budget or whose candidate exceeds 2^138 reports failure and is re-verified by the
-// full-length ladder (probability ~1e-7 per signature for uniform k).
+// the iteration budget or whose candidate exceeds 2^146 reports failure and is re-verified by the
+// full-length ladder.  max(|c|, d) has 127-128 bits typically and its tail falls ~4x per bit
+// (tests/test_lattice_host.py): ~0.15 % of k exceed 131 bits, none of 10^6 exceeded 140.
 #pragma once
 #include <stdint.h>
 
@@ -33,7 +34,7 @@ namespace lat {
 typedef uint32_t w32;
 typedef uint64_t w64;
 
-constexpr int HALF_BITS = 138;   // accepted |c|, |d| < 2^HALF_BITS
+constexpr int HALF_BITS = 146;   // accepted |c|, |d| < 2^HALF_BITS (<= 37 radix-16 windows)
 constexpr int MAX_ITERS = 192;   // Euclid steps (incl. partial-quotient steps); ~70 on average
 
 // 8l, little-endian words
@@ -132,6 +133,7 @@ struct HalfScalars {
   w32 d[5];      // d > 0, odd
   bool c_neg;    // c < 0
   bool ok;
+  int bits;      // max(bit length |c|, bit length d)
 };
 
 NWC_HD HalfScalars reduce(const w32 k[8]) {
@@ -219,8 +221,10 @@ NWC_HD HalfScalars reduce(const w32 k[8]) {
   abs5(tc, h.d);
   h.c_neg = tneg;     // (c, d) -> (-c, -d) when d < 0; c8 >= 0, so then c < 0
   for (int i = 0; i < 5; ++i) h.c[i] = c8[i];
-  const bool c_small = (c8[5] | c8[6] | c8[7]) == 0 && bitlen5(h.c) <= HALF_BITS;
-  const bool d_small = bitlen5(h.d) <= HALF_BITS;
+  const int cbits = bitlen5(h.c), dbits = bitlen5(h.d);
+  h.bits = cbits > dbits ? cbits : dbits;
+  const bool c_small = (c8[5] | c8[6] | c8[7]) == 0 && cbits <= HALF_BITS;
+  const bool d_small = dbits <= HALF_BITS;
   if (!(c_small && d_small)) h.ok = false;
   if (c8[0] == 0 && c8[1] == 0 && c8[2] == 0 && c8[3] == 0 && c8[4] == 0) h.c_neg = false;
   return h;

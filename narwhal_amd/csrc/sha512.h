@@ -5,8 +5,6 @@
 // verification (one 128-byte block: 96 message bytes + padding; messages are always the
 // 32-byte `Digest` at the crypto surface, crypto/src/lib.rs:203,214).
 //
-// 64-bit words are plain uint64_t: hipcc lowers rotations to v_alignbit_b32 pairs, the
-// three-input XORs and Ch/Maj to gfx950's v_bitop3_b32, and 64-bit adds to v_lshl_add_u64.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,7 +33,48 @@ __device__ __constant__ const uint64_t SHA512_K[80] = {
   0x28db77f523047d84ULL,0x32caab7b40c72493ULL,0x3c9ebe0a15c9bebcULL,0x431d67c49c100d4cULL,
   0x4cc5d4becb3e42b6ULL,0x597f299cfc657e2aULL,0x5fcb6fab3ad6faecULL,0x6c44198c4a475817ULL};
 
-__device__ __forceinline__ uint64_t sha_rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit words live in VGPR pairs; every rotation is two v_alignbit_b32 on the halves, every
+// three-input XOR / Ch / Maj one v_bitop3_b32 per half, every 64-bit add one v_lshl_add_u64
+// (hipcc's own lowering of (x >> n) | (x << 64 - n) used 64-bit shifts plus ORs: ~5.1k VALU
+// instructions per block against ~3.4k here).
+__device__ __forceinline__ uint32_t sha_lo(uint64_t x) { return (uint32_t)x; }
+__device__ __forceinline__ uint32_t sha_hi(uint64_t x) { return (uint32_t)(x >> 32); }
+__device__ __forceinline__ uint64_t sha_pack(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
+// rotr(x, n) as (hi, lo) for a compile-time n in 1..63, n != 32
+template <int N> __device__ __forceinline__ void sha_rotr2(uint64_t x, uint32_t& hi, uint32_t& lo) {
+  static_assert(N > 0 && N < 64 && N != 32, "rotation");
+  const uint32_t a = sha_hi(x), b = sha_lo(x);
+  if constexpr (N < 32) {
+    lo = __builtin_amdgcn_alignbit(a, b, N);
+    hi = __builtin_amdgcn_alignbit(b, a, N);
+  } else {
+    lo = __builtin_amdgcn_alignbit(b, a, N - 32);
+    hi = __builtin_amdgcn_alignbit(a, b, N - 32);
+  }
+}
+// x >> n for 0 < n < 32
+template <int N> __device__ __forceinline__ void sha_shr2(uint64_t x, uint32_t& hi, uint32_t& lo) {
+  lo = __builtin_amdgcn_alignbit(sha_hi(x), sha_lo(x), N);
+  hi = sha_hi(x) >> N;
+}
+constexpr unsigned SHA_XOR3 = 0x96, SHA_CH = 0xCA, SHA_MAJ = 0xE8;   // bitop3 truth tables (a, b, c)
+#define NWC_SHA_BITOP3(a, b, c, OP)                                                                   \
+  sha_pack(__builtin_amdgcn_bitop3_b32(sha_hi(a), sha_hi(b), sha_hi(c), OP),                          \
+           __builtin_amdgcn_bitop3_b32(sha_lo(a), sha_lo(b), sha_lo(c), OP))
+template <int A, int B, int C> __device__ __forceinline__ uint64_t sha_Sigma(uint64_t x) {
+  uint32_t h0, l0, h1, l1, h2, l2;
+  sha_rotr2<A>(x, h0, l0);
+  sha_rotr2<B>(x, h1, l1);
+  sha_rotr2<C>(x, h2, l2);
+  return sha_pack(__builtin_amdgcn_bitop3_b32(h0, h1, h2, SHA_XOR3), __builtin_amdgcn_bitop3_b32(l0, l1, l2, SHA_XOR3));
+}
+template <int A, int B, int C> __device__ __forceinline__ uint64_t sha_sigma(uint64_t x) {
+  uint32_t h0, l0, h1, l1, h2, l2;
+  sha_rotr2<A>(x, h0, l0);
+  sha_rotr2<B>(x, h1, l1);
+  sha_shr2<C>(x, h2, l2);
+  return sha_pack(__builtin_amdgcn_bitop3_b32(h0, h1, h2, SHA_XOR3), __builtin_amdgcn_bitop3_b32(l0, l1, l2, SHA_XOR3));
+}
 
 __device__ __forceinline__ void sha512_init_state(uint64_t st[8]) {
   st[0] = 0x6a09e667f3bcc908ULL; st[1] = 0xbb67ae8584caa73bULL; st[2] = 0x3c6ef372fe94f82bULL;
@@ -45,6 +84,8 @@ __device__ __forceinline__ void sha512_init_state(uint64_t st[8]) {
 
 // One compression.  The 16-word schedule window is kept in registers and updated in place
 // (w[t & 15]), so the block costs 16 live 64-bit words, not 80.
+//   Ch(e, f, g)  = (e & f) ^ (~e & g)          bitop3 0xCA
+//   Maj(a, b, c) = (a & b) ^ (a & c) ^ (b & c) bitop3 0xE8
 __device__ __forceinline__ void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll
@@ -53,17 +94,16 @@ __device__ __forceinline__ void sha512_compress(uint64_t st[8], uint64_t w[16]) 
     if (t < 16) {
       wt = w[t];
     } else {
-      const uint64_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      const uint64_t s0 = sha_rotr(w15, 1) ^ sha_rotr(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = sha_rotr(w2, 19) ^ sha_rotr(w2, 61) ^ (w2 >> 6);
+      const uint64_t s0 = sha_sigma<1, 8, 7>(w[(t - 15) & 15]);
+      const uint64_t s1 = sha_sigma<19, 61, 6>(w[(t - 2) & 15]);
       wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
       w[t & 15] = wt;
     }
-    const uint64_t S1 = sha_rotr(e, 14) ^ sha_rotr(e, 18) ^ sha_rotr(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
+    const uint64_t S1 = sha_Sigma<14, 18, 41>(e);
+    const uint64_t ch = NWC_SHA_BITOP3(e, f, g, SHA_CH);
     const uint64_t t1 = h + S1 + ch + SHA512_K[t] + wt;
-    const uint64_t S0 = sha_rotr(a, 28) ^ sha_rotr(a, 34) ^ sha_rotr(a, 39);
-    const uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
+    const uint64_t S0 = sha_Sigma<28, 34, 39>(a);
+    const uint64_t maj = NWC_SHA_BITOP3(a, b, c, SHA_MAJ);
     const uint64_t t2 = S0 + maj;
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }

@@ -15,35 +15,41 @@ import sys
 VALU_PEAK = 64 * 256 * 2.4e9  # VOP3 lane-ops/s
 
 
+def kname(full):
+    """'void nwc::k_verify<true, false>(nwc::VerifyArgs)' -> 'nwc::k_verify<true, false>'; None if not ours."""
+    n = full[5:] if full.startswith("void ") else full
+    return n.split("(")[0] if n.startswith("nwc::") else None
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
     summary = {}
     for name, r in stats.items():
-        if not name.startswith("nwc::"):
+        if kname(name) is None:
             continue
-        summary[name.split("(")[0]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+        summary[kname(name)] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                        "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
     for pmc in ("pmc_sq", "pmc_fetch"):
         path = os.path.join(src, pmc, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
-        rows = [r for r in csv.DictReader(open(path)) if r["Kernel_Name"].startswith("nwc::")]
+        rows = [r for r in csv.DictReader(open(path)) if kname(r["Kernel_Name"]) is not None]
         with open(os.path.join(dst, pmc + ".csv"), "w", newline="") as f:
             w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
             w.writeheader()
             w.writerows(rows)
         agg = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in rows:
-            agg[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            agg[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, cs in agg.items():
             d = summary.setdefault(k, {})
             for c, v in cs.items():
                 d[c] = sum(v) / len(v)
-            d["VGPR"] = int(rows[[r["Kernel_Name"].split("(")[0] for r in rows].index(k)]["VGPR_Count"])
-            d["AGPR"] = int(rows[[r["Kernel_Name"].split("(")[0] for r in rows].index(k)]["Accum_VGPR_Count"])
-            d["scratch_per_lane"] = int(rows[[r["Kernel_Name"].split("(")[0] for r in rows].index(k)]["Scratch_Size"])
+            d["VGPR"] = int(rows[[kname(r["Kernel_Name"]) for r in rows].index(k)]["VGPR_Count"])
+            d["AGPR"] = int(rows[[kname(r["Kernel_Name"]) for r in rows].index(k)]["Accum_VGPR_Count"])
+            d["scratch_per_lane"] = int(rows[[kname(r["Kernel_Name"]) for r in rows].index(k)]["Scratch_Size"])
     for k, d in summary.items():
         if "SQ_INSTS_VALU" in d and "avg_ns" in d and d.get("SQ_WAVES"):
             d["valu_insts_per_lane"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
