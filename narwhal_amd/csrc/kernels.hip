@@ -108,6 +108,31 @@ __global__ void k_build_base_table(ge_niels* table) {
   table[i] = ge_p3_to_niels(acc);
 }
 
+// Radix-2^16 basepoint tables for the half-size ladder, resident in HBM (8.4 MB; L2/MALL-warm):
+// table16[h * B16_ENTRIES + j] = j * (2^(132 h) B), h = 0, 1, j = 0..32768, affine Niels padded to
+// 128 B (8 x dwordx4, the LDS-DMA granule).  One lane per entry.
+constexpr int B16_ENTRIES = 32769;
+struct ge_niels_pad { ge_niels n; u32 pad[2]; };
+static_assert(sizeof(ge_niels_pad) == 128, "padded Niels entry");
+__global__ void k_build_base_table16(ge_niels_pad* table) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * B16_ENTRIES) return;
+  ge_p3 b = ge_base_point();
+  if (i >= B16_ENTRIES) {
+    for (int k = 0; k < BASE_SPLIT_BITS; ++k) b = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(b)));
+  }
+  const int j = i % B16_ENTRIES;
+  const ge_cached bc = ge_p3_to_cached(b);
+  ge_p3 acc = ge_p3_identity();
+  for (int bit = 15; bit >= 0; --bit) {
+    acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
+    if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, bc));
+  }
+  table[i].n = ge_p3_to_niels(acc);
+  table[i].pad[0] = 0;
+  table[i].pad[1] = 0;
+}
+
 // ------------------------------------------------------------------------------- committee cache
 // nwc_set_committee (config/src/lib.rs:154-156 Committee): per key its decode flags and the
 // 129-entry affine Niels table of j * (-A), j = 0..128, resident in L2 (15.5 KB per key).
@@ -248,8 +273,8 @@ __device__ __forceinline__ ge_p2 double_scalarmult(const LaneTable& tab, u32 kd[
 // W is wave-uniform: the smallest W in [33, 37] with |c|, d < 2^(4W-1) for every lane of the
 // wave (max(|c|, d) has 127-128 bits typically; ~9 % of waves hold a lane of 132+ bits and run
 // 34-35 windows, and only |c| or d >= 2^147 -- never seen in 10^6 samples -- leaves the
-// half-size path).  The basepoint scalar eB = d s mod l is split at 2^132 into two 17-digit
-// radix-256 strings added at the even windows w <= 32.
+// half-size path).  The basepoint scalar eB = d s mod l is split at 2^132 into two 9-digit
+// radix-2^16 strings added at the windows w = 32, 28, ..., 0 from tables in HBM.
 // Digit streams are packed so the next digit is always in the top nibble/byte of word 4 and is
 // consumed by shifting the 160-bit string left:
 //   Digits16  {w[5], top}: signed radix-16 digits of x < 2^(4W-1): digits 0..W-2 in [-8, 7] as
@@ -259,7 +284,6 @@ __device__ __forceinline__ ge_p2 double_scalarmult(const LaneTable& tab, u32 kd[
 // extended (4M) because the addition needs T; a doubling only needs (X:Y:Z) (3M).  So the last
 // add of each window feeds the next window's doublings at 3M instead of 4M.
 constexpr int HALF_WINDOWS_MIN = 33, HALF_WINDOWS_MAX = 37;
-constexpr int B_DIGITS = 17;   // radix-256 digits of each half of eB (windows 32, 30, ..., 0)
 struct Digits16 { u32 w[5]; i32 top; };
 struct Digits256 { u32 w[5]; };
 
@@ -322,6 +346,53 @@ __device__ __forceinline__ Digits256 recode256(const u32 x[5], int ndig) {
   return r;
 }
 
+// Signed radix-2^16 digits of x < 2^144 (9 digits, d in [-2^15, 2^15)) as 16-bit fields d+2^15,
+// digit 8 in the top half of word 4.  Used for the two 132-bit halves of eB (tables in HBM).
+constexpr int B16_DIGITS = 9;   // windows 32, 28, ..., 0
+struct Digits65536 { u32 w[5]; };
+__device__ __forceinline__ Digits65536 recode65536(const u32 x[5]) {
+  Digits65536 r;
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) r.w[i] = 0;
+  i32 carry = 0;
+  _Pragma("unroll") for (int i = 0; i < B16_DIGITS; ++i) {
+    const i32 v = (i32)((x[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) + carry;
+    carry = (v + 32768) >> 16;
+    const i32 d = v - (carry << 16);
+    const int pos = i + 1;
+    r.w[pos >> 1] |= (u32)(d + 32768) << (16 * (pos & 1));
+  }
+  return r;
+}
+__device__ __forceinline__ i32 next65536(Digits65536& x) {
+  const i32 d = (i32)(x.w[4] >> 16) - 32768;
+  _Pragma("unroll") for (int i = 4; i > 0; --i) x.w[i] = (x.w[i] << 16) | (x.w[i - 1] >> 16);
+  x.w[0] <<= 16;
+  return d;
+}
+
+// LDS staging of basepoint-table entries fetched by LDS-DMA (global_load_lds_dwordx4): each wave
+// owns 16 x 64 uint4; chunk c of entry e of lane l sits at stage[(8 e + c) * 64 + l], so a
+// wave's DMA instruction writes 1 KB contiguous and each lane reads its own 16 B (no conflicts).
+// The fetch is issued before the window's cached adds and consumed after them, so the HBM/L2
+// latency hides behind ~2.6k VALU instructions and no VGPR holds the entry meanwhile.
+typedef __attribute__((address_space(1))) void nwc_gvoid;
+typedef __attribute__((address_space(3))) void nwc_lvoid;
+constexpr int STAGE_U4_PER_WAVE = 16 * 64;
+__device__ __forceinline__ void stage_fetch(uint4* stage, int e, const ge_niels_pad* src) {
+  const uint4* g = reinterpret_cast<const uint4*>(src);
+  _Pragma("unroll") for (int c = 0; c < 8; ++c)
+    __builtin_amdgcn_global_load_lds((nwc_gvoid*)(g + c), (nwc_lvoid*)(stage + (8 * e + c) * 64), 16, 0, 0);
+}
+__device__ __forceinline__ ge_niels stage_read(const uint4* stage, int e) {
+  const int lane = threadIdx.x & 63;
+  union { uint4 q[8]; ge_niels_pad p; } u;
+  _Pragma("unroll") for (int c = 0; c < 8; ++c) u.q[c] = stage[(8 * e + c) * 64 + lane];
+  return u.p.n;
+}
+__device__ __forceinline__ void stage_wait() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the DMA has landed in LDS
+}
+
 // Smallest W in [33, 37] with x < 2^(4W-1) for all lanes (bits = bit length per lane); 38 if none.
 __device__ __forceinline__ int wave_windows(int bits) {
   int W = HALF_WINDOWS_MIN;
@@ -343,42 +414,46 @@ __device__ __forceinline__ void ladder_dbl4(ge_p1p1& t) {
 }
 
 __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const LaneTable& tr, Digits16 cd, Digits16 dd,
-                                                 Digits256 el, Digits256 eh, const ge_niels* sB, const ge_niels* sB2,
-                                                 int W) {
-  // Code-size discipline: the window body holds ONE doubling, ONE cached add and ONE Niels add
-  // (each in a rolled loop) so the hot loop stays inside the instruction cache.
+                                                 Digits65536 el, Digits65536 eh, const ge_niels_pad* T16,
+                                                 uint4* stage, int W) {
+  // Code-size discipline: the window body holds ONE doubling and ONE Niels add (rolled loops) and
+  // two cached adds, so the hot loop stays inside the instruction cache.
   ge_p1p1 t = ge_p1p1_identity();
-  // Entries for the current window are loaded at the end of the previous window, so their
+  // A/R entries for the current window are loaded at the end of the previous window, so their
   // latency hides behind this window's doublings and only 80 registers are in flight.
   i32 da = cd.top, dr = dd.top;
   ge_cached ea = ta.load(da), er = tr.load(dr);
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     if (w != W - 1) ladder_dbl4(t);
+    const bool bwin = (w & 3) == 0 && w < 4 * B16_DIGITS;
+    i32 d0 = 0, d1 = 0;
+    if (bwin) {
+      d0 = next65536(el);
+      d1 = next65536(eh);
+      // settle the A/R entry loads first (they landed during the doublings), so no wait placed
+      // for them below also has to wait for the DMA
+      stage_wait();
+      stage_fetch(stage, 0, T16 + (d0 < 0 ? -d0 : d0));
+      stage_fetch(stage, 1, T16 + B16_ENTRIES + (d1 < 0 ? -d1 : d1));
+    }
+    // two explicit adds (a rolled 2-iteration loop needs a selected copy of the entry: 40 more
+    // live VGPRs, which spilled)
+    t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(ea, da < 0));
+    t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
+    if (bwin) {
+      stage_wait();
 #pragma unroll 1
-    for (int side = 0; side < 2; ++side) {
-      const bool neg = side ? (dr < 0) : (da < 0);
-      ge_cached q;
-      q.YpX = fe_select(ea.YpX, er.YpX, side != 0);
-      q.YmX = fe_select(ea.YmX, er.YmX, side != 0);
-      q.Z = fe_select(ea.Z, er.Z, side != 0);
-      q.T2d = fe_select(ea.T2d, er.T2d, side != 0);
-      t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(q, neg));
+      for (int side = 0; side < 2; ++side) {
+        const i32 dd_ = side ? d1 : d0;
+        t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(stage_read(stage, side), dd_ < 0));
+      }
     }
     if (w > 0) {
       da = next16(cd);
       dr = next16(dd);
       ea = ta.load(da < 0 ? -da : da);
       er = tr.load(dr < 0 ? -dr : dr);
-    }
-    if ((w & 1) == 0 && w < 2 * B_DIGITS) {
-      const i32 d0 = next256(el), d1 = next256(eh);
-#pragma unroll 1
-      for (int side = 0; side < 2; ++side) {
-        const i32 dd_ = side ? d1 : d0;
-        const ge_niels nb = (side ? sB2 : sB)[dd_ < 0 ? -dd_ : dd_];
-        t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(nb, dd_ < 0));
-      }
     }
   }
   return ge_p1p1_to_p2(t);
@@ -388,8 +463,8 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
 // radix-256 Niels table (one add at every even window, no per-equation table or decompression).
 // ca: radix-256 digits of |c| starting at window (W-1) & ~1; c_neg flips every A entry.
 __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Digits16 dd, Digits256 ca, bool c_neg,
-                                                        const ge_niels* key_tab, Digits256 el, Digits256 eh,
-                                                        const ge_niels* sB, const ge_niels* sB2, int W) {
+                                                        const ge_niels* key_tab, Digits65536 el, Digits65536 eh,
+                                                        const ge_niels_pad* T16, uint4* stage, int W) {
   ge_p1p1 t = ge_p1p1_identity();
   i32 dr = dd.top;
   ge_cached er = tr.load(dr);
@@ -398,30 +473,31 @@ __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Dig
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     if (w != W - 1) ladder_dbl4(t);
+    const bool bwin = (w & 3) == 0 && w < 4 * B16_DIGITS;
+    i32 d0 = 0, d1 = 0;
+    if (bwin) {
+      d0 = next65536(el);
+      d1 = next65536(eh);
+      // settle the A/R entry loads first (they landed during the doublings), so no wait placed
+      // for them below also has to wait for the DMA
+      stage_wait();
+      stage_fetch(stage, 0, T16 + (d0 < 0 ? -d0 : d0));
+      stage_fetch(stage, 1, T16 + B16_ENTRIES + (d1 < 0 ? -d1 : d1));
+    }
     t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
+    if ((w & 1) == 0) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(ean, (dA < 0) != c_neg));
+    if (bwin) {
+      stage_wait();
+#pragma unroll 1
+      for (int side = 0; side < 2; ++side) {
+        const i32 dd_ = side ? d1 : d0;
+        t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(stage_read(stage, side), dd_ < 0));
+      }
+    }
     if (w > 0) {
       dr = next16(dd);
       er = tr.load(dr < 0 ? -dr : dr);
-    }
-    if ((w & 1) == 0) {
-      const bool with_b = w < 2 * B_DIGITS;
-      const i32 d0 = with_b ? next256(el) : 0, d1 = with_b ? next256(eh) : 0;
-      const int sides = with_b ? 3 : 1;
-#pragma unroll 1
-      for (int side = 0; side < sides; ++side) {
-        ge_niels nb;
-        bool neg;
-        if (side == 0) {
-          nb = ean;
-          neg = (dA < 0) != c_neg;
-        } else {
-          const i32 dd_ = side == 1 ? d0 : d1;
-          nb = (side == 1 ? sB : sB2)[dd_ < 0 ? -dd_ : dd_];
-          neg = dd_ < 0;
-        }
-        t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(nb, neg));
-      }
-      if (w > 0) {
+      if ((w & 1) == 0) {
         dA = next256(ca);
         ean = key_tab[dA < 0 ? -dA : dA];
       }
@@ -493,8 +569,8 @@ __device__ bool verify_full(const u32 mw[8], const u32 aw[8], const u32 sigw[16]
   return p.ok && eq;
 }
 
-// e_B = d * s mod l, split at 2^132 into radix-256 digit strings (el, eh)
-__device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digits256& el, Digits256& eh) {
+// e_B = d * s mod l, split at 2^132 into radix-2^16 digit strings (el, eh)
+__device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digits65536& el, Digits65536& eh) {
   u32 prod[16];
   _Pragma("unroll") for (int i = 0; i < 16; ++i) prod[i] = 0;
   _Pragma("unroll") for (int x = 0; x < 5; ++x) {
@@ -514,8 +590,8 @@ __device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digi
   lo[4] = eb[4] & ((1u << SH) - 1u);
   _Pragma("unroll") for (int i = 0; i < 4; ++i) hi[i] = (eb[4 + i] >> SH) | (i + 5 < 8 ? eb[5 + i] << (32 - SH) : 0u);
   hi[4] = 0;
-  el = recode256(lo, B_DIGITS);
-  eh = recode256(hi, B_DIGITS);
+  el = recode65536(lo);
+  eh = recode65536(hi);
 }
 
 // Half-size equation: [d]e = (d s mod l) B - c A - d R == O  (lattice.h).  Sets `fallback`
@@ -523,8 +599,8 @@ __device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digi
 // When every lane of the wave has its key in the committee cache (wave-uniform test), A comes
 // from the cache: no decompression of A, no per-equation A table, 18 Niels adds for the A term.
 template <bool CACHE>
-__device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels* sB,
-                            const ge_niels* sB2, const LaneTable& ta, const LaneTable& tr, const Committee& cm,
+__device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels_pad* T16,
+                            uint4* stage, const LaneTable& ta, const LaneTable& tr, const Committee& cm,
                             bool& fallback) {
   const int key = CACHE ? committee_lookup(cm, aw) : -1;
   if (CACHE && __all(key >= 0)) {
@@ -544,12 +620,12 @@ __device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16]
     // odd W: the top radix-256 digit of |c| (window W-1) is then < 2^3 + 1, never 128
     const int W = wave_windows(h.ok ? h.bits : 0) | 1;
     fallback = !h.ok;
-    Digits256 el, eh;
+    Digits65536 el, eh;
     base_digits(h.d, sw, el, eh);
     const Digits16 dd = recode16(h.d, W);
     const Digits256 ca = recode256(h.c, ((W - 1) >> 1) + 1);
     build_table(tr, ge_p3_neg(R[0]));
-    const ge_p2 q = half_scalarmult_cached(tr, dd, ca, h.c_neg, cm.tables + (size_t)key * 129, el, eh, sB, sB2, W);
+    const ge_p2 q = half_scalarmult_cached(tr, dd, ca, h.c_neg, cm.tables + (size_t)key * 129, el, eh, T16, stage, W);
     const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
     return ok && ident && h.ok;
   }
@@ -558,13 +634,13 @@ __device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16]
   const lat::HalfScalars h = lat::reduce(p.kw);
   const int W = wave_windows(h.ok ? h.bits : 0);
   fallback = !h.ok;
-  Digits256 el, eh;
+  Digits65536 el, eh;
   base_digits(h.d, p.sw, el, eh);
   const Digits16 cd = recode16(h.c, W), dd = recode16(h.d, W);
   // -c A = |c| * (c < 0 ? A : -A);  -d R = d * (-R)
   build_table(ta, h.c_neg ? p.A : ge_p3_neg(p.A));
   build_table(tr, ge_p3_neg(p.R));
-  const ge_p2 q = half_scalarmult(ta, tr, cd, dd, el, eh, sB, sB2, W);
+  const ge_p2 q = half_scalarmult(ta, tr, cd, dd, el, eh, T16, stage, W);
   const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
   return p.ok && ident && h.ok;
 }
@@ -585,7 +661,8 @@ struct VerifyArgs {
   uint64_t* out_bits;
   uint64_t n;
   int strict;
-  const ge_niels* base_table;   // 2 x 129 entries
+  const ge_niels* base_table;   // 2 x 129 entries (radix 256; full-length ladder)
+  const ge_niels_pad* base16;   // 2 x B16_ENTRIES entries (radix 2^16; half-size ladder)
   uint8_t* scratch;             // 2 * TAB_BYTES_PER_LANE per lane slot
   uint32_t* fb_list;
   uint32_t* fb_count;
@@ -612,8 +689,12 @@ __device__ __forceinline__ void stage_base_tables(const ge_niels* src, ge_niels*
 #endif
 template <bool HALF, bool CACHE>
 __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(VerifyArgs a) {
-  __shared__ ge_niels sB[HALF ? 2 * 129 : 129];
-  stage_base_tables(a.base_table, sB, HALF ? 2 * 129 : 129);
+  // HALF: per-wave LDS-DMA staging of radix-2^16 basepoint entries (64 KB per block);
+  // full-length ladder: the radix-256 basepoint table (15.5 KB).
+  __shared__ uint4 lds[HALF ? 4 * STAGE_U4_PER_WAVE : 129 * 30 / 4];
+  ge_niels* sB = reinterpret_cast<ge_niels*>(lds);
+  if constexpr (!HALF) stage_base_tables(a.base_table, sB, 129);
+  uint4* stage = lds + (threadIdx.x >> 6) * STAGE_U4_PER_WAVE;
   const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t* base = a.scratch + slot * 2 * TAB_BYTES_PER_LANE;
   const LaneTable ta{reinterpret_cast<uint4*>(base)};
@@ -626,7 +707,7 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
     load_inputs(a, active ? i : 0, mw, aw, sgw);
     bool fb = false;
     bool v;
-    if constexpr (HALF) v = verify_half<CACHE>(mw, aw, sgw, a.strict != 0, sB, sB + 129, ta, tr, a.committee, fb);
+    if constexpr (HALF) v = verify_half<CACHE>(mw, aw, sgw, a.strict != 0, a.base16, stage, ta, tr, a.committee, fb);
     else v = verify_full(mw, aw, sgw, a.strict != 0, sB, ta);
     if (HALF && a.force_fb_every && (i % a.force_fb_every) == 0) { fb = true; v = false; }
     v = v && active;

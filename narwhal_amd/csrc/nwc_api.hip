@@ -51,6 +51,7 @@ struct DevCtx {
   int verify_blocks_per_cu = 1;
   hipStream_t stream = nullptr;
   nwc::ge_niels* base_table = nullptr;
+  nwc::ge_niels_pad* base16 = nullptr;   // radix-2^16 basepoint tables (8.4 MB)
   // k_verify per-lane table slots; reused by every launch, so launches that use it are
   // serialised across streams with `scratch_free` (recorded after each such launch).
   uint8_t* scratch = nullptr;
@@ -106,6 +107,10 @@ int init_device(DevCtx& d) {
   HIP_TRY(hipMalloc(&d.base_table, 2 * 129 * sizeof(nwc::ge_niels)));
   HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
   hipLaunchKernelGGL(nwc::k_build_base_table, dim3(5), dim3(64), 0, d.stream, d.base_table);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMalloc(&d.base16, 2 * (size_t)nwc::B16_ENTRIES * sizeof(nwc::ge_niels_pad)));
+  hipLaunchKernelGGL(nwc::k_build_base_table16, dim3((2 * nwc::B16_ENTRIES + 255) / 256), dim3(256), 0, d.stream,
+                     d.base16);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(d.stream));
   return 0;
@@ -166,7 +171,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
   }();
   const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_slots, d.cm_slot_mask, d.cm_n};
-  nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.scratch,
+  nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base16, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
   const bool half = half_path();
   if (half) HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
@@ -320,6 +325,7 @@ void nwc_shutdown(void) {
     if (d->cm_slots) (void)hipFree(d->cm_slots);
     if (d->scratch_free) (void)hipEventDestroy(d->scratch_free);
     if (d->base_table) (void)hipFree(d->base_table);
+    if (d->base16) (void)hipFree(d->base16);
     if (d->stream) (void)hipStreamDestroy(d->stream);
   }
   g_devs.clear();

@@ -82,31 +82,50 @@ __device__ __forceinline__ void sha512_init_state(uint64_t st[8]) {
   st[6] = 0x1f83d9abfb41bd6bULL; st[7] = 0x5be0cd19137e2179ULL;
 }
 
-// One compression.  The 16-word schedule window is kept in registers and updated in place
-// (w[t & 15]), so the block costs 16 live 64-bit words, not 80.
+// One compression: 5 passes of 16 statically unrolled rounds.  Round t of pass p uses schedule
+// slot w[t & 15] = w[j] with j static, so the 16-word window stays in registers with no
+// dynamic register indexing, and the a..h roles return to their places after 16 rounds (a
+// multiple of 8); the pass loop itself stays rolled (one 16-round body in the I-cache).
 //   Ch(e, f, g)  = (e & f) ^ (~e & g)          bitop3 0xCA
 //   Maj(a, b, c) = (a & b) ^ (a & c) ^ (b & c) bitop3 0xE8
+#define NWC_SHA_ROUND(a, b, c, d, e, f, g, h, J)                                                     \
+  {                                                                                                  \
+    if (pass) {                                                                                      \
+      const uint64_t s0 = sha_sigma<1, 8, 7>(w[((J) + 1) & 15]);                                     \
+      const uint64_t s1 = sha_sigma<19, 61, 6>(w[((J) + 14) & 15]);                                  \
+      w[J] = w[J] + s0 + w[((J) + 9) & 15] + s1;                                                     \
+    }                                                                                                \
+    const uint64_t S1 = sha_Sigma<14, 18, 41>(e);                                                    \
+    const uint64_t ch = NWC_SHA_BITOP3(e, f, g, SHA_CH);                                             \
+    const uint64_t t1 = h + S1 + ch + k[J] + w[J];                                                   \
+    const uint64_t S0 = sha_Sigma<28, 34, 39>(a);                                                    \
+    const uint64_t maj = NWC_SHA_BITOP3(a, b, c, SHA_MAJ);                                           \
+    d += t1;                                                                                         \
+    h = t1 + S0 + maj;                                                                               \
+  }
 __device__ __forceinline__ void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
-  for (int t = 0; t < 80; ++t) {
-    uint64_t wt;
-    if (t < 16) {
-      wt = w[t];
-    } else {
-      const uint64_t s0 = sha_sigma<1, 8, 7>(w[(t - 15) & 15]);
-      const uint64_t s1 = sha_sigma<19, 61, 6>(w[(t - 2) & 15]);
-      wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
-      w[t & 15] = wt;
-    }
-    const uint64_t S1 = sha_Sigma<14, 18, 41>(e);
-    const uint64_t ch = NWC_SHA_BITOP3(e, f, g, SHA_CH);
-    const uint64_t t1 = h + S1 + ch + SHA512_K[t] + wt;
-    const uint64_t S0 = sha_Sigma<28, 34, 39>(a);
-    const uint64_t maj = NWC_SHA_BITOP3(a, b, c, SHA_MAJ);
-    const uint64_t t2 = S0 + maj;
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+#pragma unroll 1
+  for (int pass = 0; pass < 5; ++pass) {
+    const uint64_t* k = SHA512_K + 16 * pass;
+    NWC_SHA_ROUND(a, b, c, d, e, f, g, h, 0)
+    NWC_SHA_ROUND(h, a, b, c, d, e, f, g, 1)
+    NWC_SHA_ROUND(g, h, a, b, c, d, e, f, 2)
+    NWC_SHA_ROUND(f, g, h, a, b, c, d, e, 3)
+    NWC_SHA_ROUND(e, f, g, h, a, b, c, d, 4)
+    NWC_SHA_ROUND(d, e, f, g, h, a, b, c, 5)
+    NWC_SHA_ROUND(c, d, e, f, g, h, a, b, 6)
+    NWC_SHA_ROUND(b, c, d, e, f, g, h, a, 7)
+    NWC_SHA_ROUND(a, b, c, d, e, f, g, h, 8)
+    NWC_SHA_ROUND(h, a, b, c, d, e, f, g, 9)
+    NWC_SHA_ROUND(g, h, a, b, c, d, e, f, 10)
+    NWC_SHA_ROUND(f, g, h, a, b, c, d, e, 11)
+    NWC_SHA_ROUND(e, f, g, h, a, b, c, d, 12)
+    NWC_SHA_ROUND(d, e, f, g, h, a, b, c, 13)
+    NWC_SHA_ROUND(c, d, e, f, g, h, a, b, 14)
+    NWC_SHA_ROUND(b, c, d, e, f, g, h, a, 15)
   }
+#undef NWC_SHA_ROUND
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
