@@ -817,7 +817,7 @@ __global__ __launch_bounds__(256, 2) void k_sha512_digest32(const uint8_t* __res
       const ShaBlock r = sha_block_bytes(p, len, b);
       _Pragma("unroll") for (int j = 0; j < 16; ++j) w[j] = r.w[j];
     }
-    sha512_compress(st, w);
+    sha512_compress<true>(st, w);
   }
   uint32_t* o = reinterpret_cast<uint32_t*>(out32 + 32 * i);
   _Pragma("unroll") for (int j = 0; j < 4; ++j) {

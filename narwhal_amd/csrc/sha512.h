@@ -40,6 +40,14 @@ __device__ __constant__ const uint64_t SHA512_K[80] = {
 __device__ __forceinline__ uint32_t sha_lo(uint64_t x) { return (uint32_t)x; }
 __device__ __forceinline__ uint32_t sha_hi(uint64_t x) { return (uint32_t)(x >> 32); }
 __device__ __forceinline__ uint64_t sha_pack(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
+// 64-bit add as one opaque v_lshl_add_u64: with a plain `+`, hipcc splits x + (hi << 32 | lo) into
+// a zero-extended low add plus a high add, and moves the halves into pairs (~5 v_mov per round)
+template <bool ASM> __device__ __forceinline__ uint64_t sha_add(uint64_t x, uint64_t y) {
+  if constexpr (!ASM) return x + y;
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
 // rotr(x, n) as (hi, lo) for a compile-time n in 1..63, n != 32
 template <int N> __device__ __forceinline__ void sha_rotr2(uint64_t x, uint32_t& hi, uint32_t& lo) {
   static_assert(N > 0 && N < 64 && N != 32, "rotation");
@@ -85,46 +93,58 @@ __device__ __forceinline__ void sha512_init_state(uint64_t st[8]) {
 // One compression: 5 passes of 16 statically unrolled rounds.  Round t of pass p uses schedule
 // slot w[t & 15] = w[j] with j static, so the 16-word window stays in registers with no
 // dynamic register indexing, and the a..h roles return to their places after 16 rounds (a
-// multiple of 8); the pass loop itself stays rolled (one 16-round body in the I-cache).
+// multiple of 8).  Pass 0 (no message schedule) is peeled; passes 1-4 are one rolled loop.
 //   Ch(e, f, g)  = (e & f) ^ (~e & g)          bitop3 0xCA
 //   Maj(a, b, c) = (a & b) ^ (a & c) ^ (b & c) bitop3 0xE8
 #define NWC_SHA_ROUND(a, b, c, d, e, f, g, h, J)                                                     \
   {                                                                                                  \
-    if (pass) {                                                                                      \
+    if (SCHED) {                                                                                     \
       const uint64_t s0 = sha_sigma<1, 8, 7>(w[((J) + 1) & 15]);                                     \
       const uint64_t s1 = sha_sigma<19, 61, 6>(w[((J) + 14) & 15]);                                  \
-      w[J] = w[J] + s0 + w[((J) + 9) & 15] + s1;                                                     \
+      w[J] = sha_add<ASM>(sha_add<ASM>(w[J], s0), sha_add<ASM>(w[((J) + 9) & 15], s1));                             \
     }                                                                                                \
     const uint64_t S1 = sha_Sigma<14, 18, 41>(e);                                                    \
     const uint64_t ch = NWC_SHA_BITOP3(e, f, g, SHA_CH);                                             \
-    const uint64_t t1 = h + S1 + ch + k[J] + w[J];                                                   \
+    const uint64_t t1 = sha_add<ASM>(sha_add<ASM>(h, k[J] + w[J]), sha_add<ASM>(S1, ch));                             \
     const uint64_t S0 = sha_Sigma<28, 34, 39>(a);                                                    \
     const uint64_t maj = NWC_SHA_BITOP3(a, b, c, SHA_MAJ);                                           \
-    d += t1;                                                                                         \
-    h = t1 + S0 + maj;                                                                               \
+    d = sha_add<ASM>(d, t1);                                                                              \
+    h = sha_add<ASM>(t1, sha_add<ASM>(S0, maj));                                                               \
   }
-__device__ __forceinline__ void sha512_compress(uint64_t st[8], uint64_t w[16]) {
+#define NWC_SHA_16ROUNDS                                                                              \
+  NWC_SHA_ROUND(a, b, c, d, e, f, g, h, 0)                                                           \
+  NWC_SHA_ROUND(h, a, b, c, d, e, f, g, 1)                                                           \
+  NWC_SHA_ROUND(g, h, a, b, c, d, e, f, 2)                                                           \
+  NWC_SHA_ROUND(f, g, h, a, b, c, d, e, 3)                                                           \
+  NWC_SHA_ROUND(e, f, g, h, a, b, c, d, 4)                                                           \
+  NWC_SHA_ROUND(d, e, f, g, h, a, b, c, 5)                                                           \
+  NWC_SHA_ROUND(c, d, e, f, g, h, a, b, 6)                                                           \
+  NWC_SHA_ROUND(b, c, d, e, f, g, h, a, 7)                                                           \
+  NWC_SHA_ROUND(a, b, c, d, e, f, g, h, 8)                                                           \
+  NWC_SHA_ROUND(h, a, b, c, d, e, f, g, 9)                                                           \
+  NWC_SHA_ROUND(g, h, a, b, c, d, e, f, 10)                                                          \
+  NWC_SHA_ROUND(f, g, h, a, b, c, d, e, 11)                                                          \
+  NWC_SHA_ROUND(e, f, g, h, a, b, c, d, 12)                                                          \
+  NWC_SHA_ROUND(d, e, f, g, h, a, b, c, 13)                                                          \
+  NWC_SHA_ROUND(c, d, e, f, g, h, a, b, 14)                                                          \
+  NWC_SHA_ROUND(b, c, d, e, f, g, h, a, 15)
+// ASM = true (the digest kernel): opaque 64-bit adds, -18 % instructions per block.  The verify
+// kernels keep plain adds (ASM = false): their one challenge block is ~1 % of a verification,
+// and the opaque adds cost them registers (more spills in the prologue).
+template <bool ASM = false> __device__ __forceinline__ void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll 1
-  for (int pass = 0; pass < 5; ++pass) {
-    const uint64_t* k = SHA512_K + 16 * pass;
-    NWC_SHA_ROUND(a, b, c, d, e, f, g, h, 0)
-    NWC_SHA_ROUND(h, a, b, c, d, e, f, g, 1)
-    NWC_SHA_ROUND(g, h, a, b, c, d, e, f, 2)
-    NWC_SHA_ROUND(f, g, h, a, b, c, d, e, 3)
-    NWC_SHA_ROUND(e, f, g, h, a, b, c, d, 4)
-    NWC_SHA_ROUND(d, e, f, g, h, a, b, c, 5)
-    NWC_SHA_ROUND(c, d, e, f, g, h, a, b, 6)
-    NWC_SHA_ROUND(b, c, d, e, f, g, h, a, 7)
-    NWC_SHA_ROUND(a, b, c, d, e, f, g, h, 8)
-    NWC_SHA_ROUND(h, a, b, c, d, e, f, g, 9)
-    NWC_SHA_ROUND(g, h, a, b, c, d, e, f, 10)
-    NWC_SHA_ROUND(f, g, h, a, b, c, d, e, 11)
-    NWC_SHA_ROUND(e, f, g, h, a, b, c, d, 12)
-    NWC_SHA_ROUND(d, e, f, g, h, a, b, c, 13)
-    NWC_SHA_ROUND(c, d, e, f, g, h, a, b, 14)
-    NWC_SHA_ROUND(b, c, d, e, f, g, h, a, 15)
+  {
+    constexpr bool SCHED = false;   // rounds 0..15 use the message words as they are
+    const uint64_t* k = SHA512_K;
+    NWC_SHA_16ROUNDS
   }
+#pragma unroll 1
+  for (int pass = 1; pass < 5; ++pass) {
+    constexpr bool SCHED = true;
+    const uint64_t* k = SHA512_K + 16 * pass;
+    NWC_SHA_16ROUNDS
+  }
+#undef NWC_SHA_16ROUNDS
 #undef NWC_SHA_ROUND
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
