@@ -13,7 +13,8 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnwc.so")
+# NWC_LIB_PATH: an alternative in-tree build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("NWC_LIB_PATH") or os.path.join(HERE, "libnwc.so")
 
 NWC_OK = 0
 NWC_INVALID = 1

@@ -138,6 +138,22 @@ FE_DEV fe fe_from_words(const u32 w[8]) {
   return r;
 }
 
+// Tight form of an element whose limbs are in [0, 2^w) (fe_from_words output): one carry pass
+// moving each limb into [-2^(w-1), 2^(w-1)] (+1).  Decoded coordinates are tightened so that every
+// coordinate the group formulas see meets the tight bound (2x a tight limb times 19 stays < 2^31).
+FE_DEV fe fe_tighten(const fe& f) {
+  fe r;
+  i32 c = 0;
+  _Pragma("unroll") for (int i = 0; i < 10; ++i) {
+    const int w = (i & 1) ? 25 : 26;
+    const i32 v = f.v[i] + c;
+    c = (v + (1 << (w - 1))) >> w;
+    r.v[i] = v - (c << w);
+  }
+  r.v[0] += 19 * c;
+  return r;
+}
+
 // Canonical encoding (value mod p in [0, p)) as 8 little-endian words.
 // Bias by 16p so every limb is non-negative, two carry passes bring every limb into range
 // (the second can only ripple out of limb 0), then subtract p once if value >= p.

@@ -164,10 +164,11 @@ FE_DEV void ge_decompressN(ge_p3 out[N], const u32* const w[N], u32 ycanon[N][8]
     r = fe_select(r, fe_neg(r), fe_is_negative(r));
     const bool sign = (w[k][7] >> 31) & 1;
     const fe x = fe_select(r, fe_neg(r), sign);
+    const fe yt = fe_tighten(y[k]);
     out[k].X = x;
-    out[k].Y = y[k];
+    out[k].Y = yt;
     out[k].Z = one;
-    out[k].T = fe_mul(x, y[k]);
+    out[k].T = fe_mul(x, yt);
     fe_to_words(y[k], ycanon[k]);
     ok[k] = correct || flipped;
   }

@@ -401,8 +401,15 @@ __device__ __forceinline__ int wave_windows(int bits) {
   return W;
 }
 
-__device__ __forceinline__ ge_p1p1 ge_p1p1_identity() {
-  ge_p1p1 r; r.X = fe_zero(); r.Y = fe_one(); r.Z = fe_one(); r.T = fe_one(); return r;
+// A cached entry (Y+X, Y-X, Z, 2dT) as a completed point: (2X : 2Y : 2Z : 2Z) -- the ladder's first
+// window starts from its first entry instead of adding it to the identity (one add saved).
+__device__ __forceinline__ ge_p1p1 ge_cached_to_p1p1(const ge_cached& c) {
+  ge_p1p1 r;
+  r.X = fe_sub(c.YpX, c.YmX);
+  r.Y = fe_add(c.YpX, c.YmX);
+  r.Z = fe_add(c.Z, c.Z);
+  r.T = r.Z;
+  return r;
 }
 
 // four doublings of t (t in, t out), (X:Y:Z) only
@@ -418,11 +425,11 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
                                                  uint4* stage, int W) {
   // Code-size discipline: the window body holds ONE doubling and ONE Niels add (rolled loops) and
   // two cached adds, so the hot loop stays inside the instruction cache.
-  ge_p1p1 t = ge_p1p1_identity();
   // A/R entries for the current window are loaded at the end of the previous window, so their
   // latency hides behind this window's doublings and only 80 registers are in flight.
-  i32 da = cd.top, dr = dd.top;
+  i32 da = cd.top, dr = dd.top;   // top digits are >= 0
   ge_cached ea = ta.load(da), er = tr.load(dr);
+  ge_p1p1 t = ge_cached_to_p1p1(ea);
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     if (w != W - 1) ladder_dbl4(t);
@@ -439,7 +446,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
     }
     // two explicit adds (a rolled 2-iteration loop needs a selected copy of the entry: 40 more
     // live VGPRs, which spilled)
-    t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(ea, da < 0));
+    if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(ea, da < 0));
     t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
     if (bwin) {
       stage_wait();
@@ -465,9 +472,9 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
 __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Digits16 dd, Digits256 ca, bool c_neg,
                                                         const ge_niels* key_tab, Digits65536 el, Digits65536 eh,
                                                         const ge_niels_pad* T16, uint4* stage, int W) {
-  ge_p1p1 t = ge_p1p1_identity();
-  i32 dr = dd.top;
+  i32 dr = dd.top;   // >= 0
   ge_cached er = tr.load(dr);
+  ge_p1p1 t = ge_cached_to_p1p1(er);
   i32 dA = next256(ca);
   ge_niels ean = key_tab[dA < 0 ? -dA : dA];
 #pragma unroll 1
@@ -484,7 +491,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Dig
       stage_fetch(stage, 0, T16 + (d0 < 0 ? -d0 : d0));
       stage_fetch(stage, 1, T16 + B16_ENTRIES + (d1 < 0 ? -d1 : d1));
     }
-    t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
+    if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
     if ((w & 1) == 0) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(ean, (dA < 0) != c_neg));
     if (bwin) {
       stage_wait();
@@ -725,8 +732,9 @@ template __global__ void k_verify<false, false>(VerifyArgs);
 // Full-length re-verification of the lanes k_verify could not reduce (rare); sets their bits.
 __global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {
   __shared__ ge_niels sB[129];
-  stage_base_tables(a.base_table, sB, 129);
   const uint32_t count = *a.fb_count;
+  if (count == 0) return;   // the usual case: no table staging, ~2 us
+  stage_base_tables(a.base_table, sB, 129);
   const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const LaneTable ta{reinterpret_cast<uint4*>(a.scratch + slot * 2 * TAB_BYTES_PER_LANE)};
   for (uint32_t j = (uint32_t)slot; j < count; j += gridDim.x * blockDim.x) {
