@@ -55,6 +55,26 @@ CFG4_BATCH_BYTES = 12 + CFG4_TXS * (8 + CFG4_TX_BYTES)   # 508,052
 CFG4_STRIDE = (CFG4_BATCH_BYTES + 255) & ~255
 
 
+PROFILE_ROUND = "r01"   # profiles/<round>/summary.json: rocprofv3 PMC passes of this build
+
+
+def profile_counters(kernel_prefix: str):
+    """Per-launch PMC figures of `kernel_prefix` from the committed rocprofv3 summary
+    (tools/profile_round.sh -> tools/summarize_profile.py): HBM traffic = FETCH_SIZE x2 (gfx950
+    wide-read correction) + WRITE_SIZE, and the hardware VALU issue fraction.  None if absent."""
+    path = os.path.join(ROOT, "profiles", PROFILE_ROUND, "summary.json")
+    try:
+        summ = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    for k, d in summ.items():
+        if k.startswith(kernel_prefix) and "hbm_traffic_bytes_per_launch" in d:
+            return {"traffic": d["hbm_traffic_bytes_per_launch"], "valu_issue_frac": d.get("valu_issue_frac"),
+                    "valu_insts_per_wave": d.get("valu_insts_per_lane"), "avg_ns": d.get("avg_ns"),
+                    "source": "profiles/%s/summary.json (%s)" % (PROFILE_ROUND, k)}
+    return None
+
+
 def ops_per_verify() -> float:
     return W_S * OPS_S + W_M * OPS_M + W_SHA * OPS_SHA
 
@@ -367,6 +387,12 @@ def main():
         if digest is not None:
             digest["cpu_baseline"] = cpu_baseline_digest(args.cpu_budget / 2)
 
+    vpc = profile_counters("nwc::k_verify<true, false>")
+    dpc = profile_counters("nwc::k_sha512_digest32")
+    if digest is not None and dpc:
+        digest["traffic"] = dpc["traffic"]
+        digest["hw_valu_issue_frac"] = dpc["valu_issue_frac"]
+        digest["pmc_source"] = dpc["source"]
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
@@ -379,7 +405,13 @@ def main():
                        "verdicts_ok": ok, "verdict_allgather_ms": gather_ms,
                        "allgather_needed": False},
             "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
-                         "frac": achieved_tops / VALU_PEAK_TOPS, "traffic": None,
+                         "frac": achieved_tops / VALU_PEAK_TOPS,
+                         "frac_kind": "effective (dalek work model; the half-size ladder does less work, so >1 "
+                                      "is possible); hw_valu_issue_frac is the counter-measured fraction",
+                         "traffic": vpc["traffic"] if vpc else None,
+                         "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)",
+                         "hw_valu_issue_frac": vpc["valu_issue_frac"] if vpc else None,
+                         "pmc_source": vpc["source"] if vpc else None,
                          "kernel": "k_verify", "kernel_ms": kernel_ms,
                          "ops_per_verify": ops_per_verify(),
                          "work_model": "%d S + %d M + %d SHA-512 block per verify (dalek op model) x "

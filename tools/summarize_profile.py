@@ -31,7 +31,7 @@ def main(src, dst):
             continue
         summary[kname(name)] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                        "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
-    for pmc in ("pmc_sq", "pmc_fetch"):
+    for pmc in ("pmc_sq", "pmc_fetch", "pmc_write", "pmc_clk"):
         path = os.path.join(src, pmc, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
@@ -58,6 +58,14 @@ def main(src, dst):
         if "FETCH_SIZE" in d:
             d["fetch_bytes_reported"] = d["FETCH_SIZE"] * 1024
             d["fetch_bytes_x2_gfx950"] = d["FETCH_SIZE"] * 1024 * 2
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            # MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE (KB) x2 on gfx950 for 16-B/lane reads,
+            # WRITE_SIZE (KB) exact for 16-B/lane stores; per launch (counters are per dispatch)
+            d["write_bytes"] = d["WRITE_SIZE"] * 1024
+            d["hbm_traffic_bytes_per_launch"] = d["fetch_bytes_x2_gfx950"] + d["write_bytes"]
+        if "GRBM_GUI_ACTIVE" in d and "avg_ns" in d:
+            # GRBM_GUI_ACTIVE comes back summed over the 8 XCD instances
+            d["gui_active_clk_ghz_per_xcd"] = d["GRBM_GUI_ACTIVE"] / 8 / d["avg_ns"]
     json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
