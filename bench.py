@@ -58,7 +58,7 @@ CFG4_STRIDE = (CFG4_BATCH_BYTES + 255) & ~255
 PROFILE_ROUND = "r01"   # profiles/<round>/summary.json: rocprofv3 PMC passes of this build
 
 
-def profile_counters(kernel_prefix: str):
+def profile_counters(*kernel_names: str):
     """Per-launch PMC figures of `kernel_prefix` from the committed rocprofv3 summary
     (tools/profile_round.sh -> tools/summarize_profile.py): HBM traffic = FETCH_SIZE x2 (gfx950
     wide-read correction) + WRITE_SIZE, and the hardware VALU issue fraction.  None if absent."""
@@ -67,8 +67,9 @@ def profile_counters(kernel_prefix: str):
         summ = json.load(open(path))
     except (OSError, ValueError):
         return None
-    for k, d in summ.items():
-        if k.startswith(kernel_prefix) and "hbm_traffic_bytes_per_launch" in d:
+    for k in kernel_names:
+        d = summ.get(k, {})
+        if "hbm_traffic_bytes_per_launch" in d:
             return {"traffic": d["hbm_traffic_bytes_per_launch"], "valu_issue_frac": d.get("valu_issue_frac"),
                     "valu_insts_per_wave": d.get("valu_insts_per_lane"), "avg_ns": d.get("avg_ns"),
                     "source": "profiles/%s/summary.json (%s)" % (PROFILE_ROUND, k)}
@@ -163,27 +164,37 @@ def cfg4_host_batch(b: int) -> bytes:
 
 def bench_cfg1(lib, calls: int = 2000):
     """BASELINE config 1: Signature::verify_batch on a 4-node certificate (3 votes, 32-byte
-    digest) through the host ABI (H2D + kernel + D2H per call).  Latency-bound by design."""
+    digest) through the host ABI (H2D + kernel + D2H per call).  Latency-bound by design.
+    Timed without and with the committee cache (the 4 authorities' keys, as a node always has
+    its committee: config/src/lib.rs Committee); the cached leg runs the latency kernel."""
     from narwhal_amd import _lib, device
     import torch
     n = 3
-    seeds = device.derive32(b"nw-cfg1-key", 0, n)
+    seeds = device.derive32(b"nw-cfg1-key", 0, n + 1)
     digest = device.derive32(b"nw-cfg1-digest", 0, 1)
-    pks, sigs = device.keygen_sign(seeds, digest.repeat(n, 1))
+    allpk, _ = device.keygen_sign(seeds, digest.repeat(n + 1, 1))
+    pks, sigs = device.keygen_sign(seeds[:n].contiguous(), digest.repeat(n, 1))
     torch.cuda.synchronize()
     d, p, s = (t.cpu().numpy().tobytes() for t in (digest, pks, sigs))
-    lat = []
-    for i in range(calls + 50):
-        t0 = time.perf_counter()
-        rc = lib.nwc_verify_batch(_lib.buf(d), _lib.buf(p), _lib.buf(s), n, None)
-        dt = time.perf_counter() - t0
-        assert rc == 0, rc
-        if i >= 50:
-            lat.append(dt)
-    lat = np.array(lat) * 1e6
-    return {"workload": "cfg1: verify_batch, 3 votes, host ABI incl. H2D/D2H", "calls": calls,
-            "p50_us": float(np.percentile(lat, 50)), "p99_us": float(np.percentile(lat, 99)),
-            "calls_per_s": float(1e6 / lat.mean())}
+    committee = allpk.cpu().numpy()
+    out = {"workload": "cfg1: verify_batch, 3 votes of a 4-node committee, host ABI incl. H2D/D2H"}
+    for tag, cache in (("no_cache", False), ("cache", True)):
+        if cache:
+            _lib.check(lib.nwc_set_committee(_lib.buf(committee), n + 1))
+        lat = []
+        for i in range(calls + 50):
+            t0 = time.perf_counter()
+            rc = lib.nwc_verify_batch(_lib.buf(d), _lib.buf(p), _lib.buf(s), n, None)
+            dt = time.perf_counter() - t0
+            assert rc == 0, rc
+            if i >= 50:
+                lat.append(dt)
+        if cache:
+            _lib.check(lib.nwc_set_committee(None, 0))
+        lat = np.array(lat) * 1e6
+        out[tag] = {"calls": calls, "p50_us": float(np.percentile(lat, 50)),
+                    "p99_us": float(np.percentile(lat, 99)), "calls_per_s": float(1e6 / lat.mean())}
+    return out
 
 
 def bench_cfg3(lib, m: int, steps: int):
@@ -387,7 +398,7 @@ def main():
         if digest is not None:
             digest["cpu_baseline"] = cpu_baseline_digest(args.cpu_budget / 2)
 
-    vpc = profile_counters("nwc::k_verify<true, false>")
+    vpc = profile_counters("nwc::k_verify<true, false, false>", "nwc::k_verify<true, false>")
     dpc = profile_counters("nwc::k_sha512_digest32")
     if digest is not None and dpc:
         digest["traffic"] = dpc["traffic"]

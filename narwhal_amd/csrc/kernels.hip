@@ -143,6 +143,7 @@ struct Committee {
   const u32* keys;          // n x 8 words: the raw 32-byte keys
   const u32* flags;         // n: bit0 = decodes, bit1 = small-order
   const ge_niels* tables;   // n x 129
+  const ge_niels_pad* comb;   // n x COMB_PER_KEY (nullptr: committee too large for combs)
   const int32_t* slots;     // hash slot -> key index, -1 = empty
   u32 slot_mask;            // slots - 1 (power of two)
   u32 n;
@@ -188,6 +189,44 @@ __global__ void k_build_key_tables(const u32* __restrict__ keys, u32 n, ge_niels
   }
   tables[(size_t)key * 129 + j] = ge_p3_to_niels(acc);
   if (j == 0) flags[key] = (ok[0] ? 1u : 0u) | (ycanon_is_small_order(yc[0]) ? 2u : 0u);
+}
+
+// ------------------------------------------------------------------------------- committee combs
+// Fixed-base combs for the doubling-free committee path (k_verify_comb): for a point P,
+//   comb[w * 129 + j] = j * 256^w * P,   w = 0..31, j = 0..128   (affine Niels, 128-B entries)
+// so that x * P = sum_w comb[w][d_w] (signed: a negative digit negates the entry) for the signed
+// radix-256 digits d_w of any x < 2^253.  P = B for the basepoint comb (528 KB, built at
+// nwc_init) and P = -A_key for each committee key (528 KB per key, built by nwc_set_committee).
+// One lane per entry: 8w doublings of P, an 8-bit double-and-add, one inversion.
+constexpr int COMB_WINDOWS = 32, COMB_ENTRIES = 129;
+constexpr size_t COMB_PER_KEY = (size_t)COMB_WINDOWS * COMB_ENTRIES;
+__global__ void k_build_comb(const u32* __restrict__ keys, u32 n, ge_niels_pad* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)(keys ? n : 1u) * COMB_PER_KEY) return;
+  const u32 key = (u32)(t / COMB_PER_KEY), r = (u32)(t % COMB_PER_KEY);
+  const int w = (int)(r / COMB_ENTRIES), j = (int)(r % COMB_ENTRIES);
+  ge_p3 P;
+  if (keys) {
+    u32 kw[8];
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) kw[i] = keys[8 * key + i];
+    u32 yc[1][8];
+    bool ok[1];
+    const u32* const wp[1] = {kw};
+    ge_decompressN<1>(&P, wp, yc, ok);
+    P = ge_p3_neg(P);
+  } else {
+    P = ge_base_point();
+  }
+  for (int k = 0; k < 8 * w; ++k) P = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
+  const ge_cached pc = ge_p3_to_cached(P);
+  ge_p3 acc = ge_p3_identity();
+  for (int bit = 7; bit >= 0; --bit) {
+    acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
+    if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, pc));
+  }
+  out[t].n = ge_p3_to_niels(acc);
+  out[t].pad[0] = 0;
+  out[t].pad[1] = 0;
 }
 
 // ------------------------------------------------------------------------------- ladder
@@ -606,7 +645,7 @@ __device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digi
 // When every lane of the wave has its key in the committee cache (wave-uniform test), A comes
 // from the cache: no decompression of A, no per-equation A table, 18 Niels adds for the A term.
 template <bool CACHE>
-__device__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels_pad* T16,
+__device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels_pad* T16,
                             uint4* stage, const LaneTable& ta, const LaneTable& tr, const Committee& cm,
                             bool& fallback) {
   const int key = CACHE ? committee_lookup(cm, aw) : -1;
@@ -676,6 +715,15 @@ struct VerifyArgs {
   uint32_t force_fb_every;      // test hook: route equations i % every == 0 to the fallback (0 = off)
   Committee committee;          // n == 0: no cache
 };
+// Extra arguments of the comb path (kept out of VerifyArgs so the headline kernel's argument
+// block and register allocation do not change).
+//   list mode (k_verify<.., LIST>): process equations list[0 .. *count) and OR their verdict bits
+//   into out_bits;  k_verify_comb: appends equations whose key is not cached to list / count.
+struct CombArgs {
+  uint32_t* list;
+  uint32_t* count;
+  const ge_niels_pad* comb_base;   // basepoint comb (COMB_PER_KEY entries)
+};
 
 __device__ __forceinline__ void load_inputs(const VerifyArgs& a, uint64_t i, u32 mw[8], u32 aw[8], u32 sgw[16]) {
   const uint64_t mi = a.msg_index ? (uint64_t)a.msg_index[i] : i * a.msg_stride;
@@ -694,8 +742,8 @@ __device__ __forceinline__ void stage_base_tables(const ge_niels* src, ge_niels*
 #ifndef NWC_VERIFY_WAVES_PER_SIMD
 #define NWC_VERIFY_WAVES_PER_SIMD 2
 #endif
-template <bool HALF, bool CACHE>
-__global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(VerifyArgs a) {
+template <bool HALF, bool CACHE, bool LIST = false>
+__global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(VerifyArgs a, CombArgs ca) {
   // HALF: per-wave LDS-DMA staging of radix-2^16 basepoint entries (64 KB per block);
   // full-length ladder: the radix-256 basepoint table (15.5 KB).
   __shared__ uint4 lds[HALF ? 4 * STAGE_U4_PER_WAVE : 129 * 30 / 4];
@@ -707,9 +755,11 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
   const LaneTable ta{reinterpret_cast<uint4*>(base)};
   const LaneTable tr{reinterpret_cast<uint4*>(base + TAB_BYTES_PER_LANE)};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < a.n; b0 += stride) {
-    const uint64_t i = b0 + threadIdx.x;
-    const bool active = i < a.n;
+  const uint64_t n = LIST ? (uint64_t)*ca.count : a.n;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < n; b0 += stride) {
+    const uint64_t idx = b0 + threadIdx.x;
+    const bool active = idx < n;
+    const uint64_t i = LIST ? (active ? (uint64_t)ca.list[idx] : 0) : idx;
     u32 mw[8], aw[8], sgw[16];
     load_inputs(a, active ? i : 0, mw, aw, sgw);
     bool fb = false;
@@ -720,14 +770,19 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
     v = v && active;
     fb = fb && active;
     if (fb) a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)i;
-    const uint64_t ballot = __ballot(v);
-    if ((threadIdx.x & 63) == 0 && b0 + (threadIdx.x & ~63u) < a.n) a.out_bits[(b0 + threadIdx.x) >> 6] = ballot;
+    if constexpr (LIST) {
+      if (v) atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));
+    } else {
+      const uint64_t ballot = __ballot(v);
+      if ((threadIdx.x & 63) == 0 && b0 + (threadIdx.x & ~63u) < n) a.out_bits[(b0 + threadIdx.x) >> 6] = ballot;
+    }
   }
 }
 
-template __global__ void k_verify<true, false>(VerifyArgs);
-template __global__ void k_verify<true, true>(VerifyArgs);
-template __global__ void k_verify<false, false>(VerifyArgs);
+template __global__ void k_verify<true, false>(VerifyArgs, CombArgs);
+template __global__ void k_verify<true, true>(VerifyArgs, CombArgs);
+template __global__ void k_verify<false, false>(VerifyArgs, CombArgs);
+template __global__ void k_verify<true, false, true>(VerifyArgs, CombArgs);
 
 // Full-length re-verification of the lanes k_verify could not reduce (rare); sets their bits.
 __global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {
@@ -743,6 +798,214 @@ __global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {
     load_inputs(a, i, mw, aw, sgw);
     if (verify_full(mw, aw, sgw, a.strict != 0, sB, ta))
       atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));
+  }
+}
+
+// ------------------------------------------------------------------------------- committee comb verify
+// Doubling-free verification for equations whose key is in the committee cache:
+//   R' = s B + k (-A) = sum_w combB[w][s_w] + sum_w combA_key[w][k_w]      (64 Niels adds)
+// and R' == R is decided on the compressed form: y(R') == y_R mod p and sign(x(R')) == bit 255 of
+// R (any sign when x(R') = 0, since dalek decodes -0 as 0).  This is exactly dalek's decision
+// "R decodes and R' == R as points": if the encodings agree, R decodes to R'; if R does not decode
+// no point has its y.  Small-order R (strict) is read off the canonical y of the encoding (every
+// small-order y decodes).  Compressing needs 1/Z; the lane batches the inversions of COMB_BATCH
+// equations (Montgomery: one exponentiation + 3 multiplications each) -- a decompression of R, the
+// alternative, is a square root and cannot be batched.
+// Equations whose key is not cached go to uc_list and are verified by k_verify in list mode.
+struct CombRec { fe X, Y, Z, P; u32 yr[8]; u32 meta; u32 pad[3]; };
+static_assert(sizeof(CombRec) == 208, "comb record layout");
+constexpr int COMB_BATCH = 8;
+constexpr size_t COMB_REC_U4 = sizeof(CombRec) / 16;
+constexpr size_t COMB_BYTES_PER_LANE = COMB_BATCH * sizeof(CombRec);
+
+__device__ __forceinline__ ge_niels comb_load(const ge_niels_pad* tab, int w, i32 d) {
+  const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)w * COMB_ENTRIES + (d < 0 ? -d : d));
+  union { uint4 u[8]; ge_niels_pad p; } e;
+  _Pragma("unroll") for (int c = 0; c < 8; ++c) e.u[c] = q[c];
+  return e.p.n;
+}
+__device__ __forceinline__ void rec_store(uint4* base, int j, const CombRec& r) {
+  const uint4* src = reinterpret_cast<const uint4*>(&r);
+  _Pragma("unroll") for (size_t c = 0; c < COMB_REC_U4; ++c) base[j * COMB_REC_U4 + c] = src[c];
+}
+__device__ __forceinline__ CombRec rec_load(const uint4* base, int j) {
+  CombRec r;
+  uint4* dst = reinterpret_cast<uint4*>(&r);
+  _Pragma("unroll") for (size_t c = 0; c < COMB_REC_U4; ++c) dst[c] = base[j * COMB_REC_U4 + c];
+  return r;
+}
+// affine Niels entry as a completed point (2x : 2y : 2 : 2) -- starts the sum without an add
+__device__ __forceinline__ ge_p1p1 ge_niels_to_p1p1(const ge_niels& q) {
+  ge_p1p1 r;
+  r.X = fe_sub(q.ypx, q.ymx);
+  r.Y = fe_add(q.ypx, q.ymx);
+  r.Z = fe_zero(); r.Z.v[0] = 2;
+  r.T = r.Z;
+  return r;
+}
+
+// s B + k (-A) over the two combs; returns (X:Y:Z)
+__device__ __forceinline__ ge_p2 comb_sum(const u32 sw[8], const u32 kw[8], const ge_niels_pad* TB,
+                                          const ge_niels_pad* TA) {
+  u32 sd[8], kd[8];
+  sc_recode_radix256(sw, sd);
+  sc_recode_radix256(kw, kd);
+  i32 ds = (i32)(sd[7] >> 24) - 128;
+  i32 dk = (i32)(kd[7] >> 24) - 128;
+  digits_shl(sd, 8);
+  digits_shl(kd, 8);
+  ge_niels nb = comb_load(TB, 31, ds);
+  ge_niels na = comb_load(TA, 31, dk);
+  ge_p1p1 t = ge_niels_to_p1p1(ge_niels_cneg(nb, ds < 0));
+#pragma unroll 1
+  for (int w = 31; w >= 0; --w) {
+    if (w != 31) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(nb, ds < 0));
+    const i32 dk_cur = dk;
+    if (w > 0) {
+      ds = (i32)(sd[7] >> 24) - 128;
+      digits_shl(sd, 8);
+      nb = comb_load(TB, w - 1, ds);
+    }
+    t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(na, dk_cur < 0));
+    if (w > 0) {
+      dk = (i32)(kd[7] >> 24) - 128;
+      digits_shl(kd, 8);
+      na = comb_load(TA, w - 1, dk);
+    }
+  }
+  return ge_p1p1_to_p2(t);
+}
+
+__global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs ca) {
+  const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint4* recs = reinterpret_cast<uint4*>(a.scratch + slot * COMB_BYTES_PER_LANE);
+  const Committee& cm = a.committee;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x; c0 < a.n; c0 += stride * COMB_BATCH) {
+    // forward: R' of up to COMB_BATCH equations, running product of their Z
+    fe P = fe_one();
+    int nb = 0;
+#pragma unroll 1
+    for (int j = 0; j < COMB_BATCH; ++j) {
+      const uint64_t b0 = c0 + (uint64_t)j * stride;
+      if (b0 >= a.n) break;   // block-uniform
+      const uint64_t i = b0 + threadIdx.x;
+      const bool active = i < a.n;
+      u32 mw[8], aw[8], sgw[16];
+      load_inputs(a, active ? i : 0, mw, aw, sgw);
+      const int key = committee_lookup(cm, aw);
+      if (active && key < 0) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;
+      const int kk = key < 0 ? 0 : key;
+      u32 rw[8], sw[8];
+      _Pragma("unroll") for (int q = 0; q < 8; ++q) { rw[q] = sgw[q]; sw[q] = sgw[8 + q]; }
+      CombRec r;
+      fe_to_words(fe_from_words(rw), r.yr);   // y_R mod p
+      const u32 fl = cm.flags[kk];
+      const bool small = a.strict && (((fl >> 1) & 1) || ycanon_is_small_order(r.yr));
+      const bool ok = active && key >= 0 && sc_lt_l(sw) && (fl & 1) && !small;
+      u32 kw[8];
+      challenge(rw, aw, mw, kw);
+      const ge_p2 q = comb_sum(sw, kw, ca.comb_base, cm.comb + (size_t)kk * COMB_PER_KEY);
+      // Z != 0 for every sum of curve points (complete formulas); a key that does not decode has
+      // an off-curve comb, whose Z must not zero the lane's batched inversion
+      const bool zbad = fe_is_zero(q.Z);
+      r.X = q.X; r.Y = q.Y; r.Z = fe_select(q.Z, fe_one(), zbad); r.P = P;
+      r.meta = (ok && !zbad ? 1u : 0u) | ((rw[7] >> 31) << 1);
+      r.pad[0] = r.pad[1] = r.pad[2] = 0;
+      rec_store(recs, j, r);
+      P = fe_mul(P, r.Z);
+      nb = j + 1;
+    }
+    // one inversion for the lane's nb equations, then backwards: 1/Z_j = inv * P_{j-1}
+    fe inv = fe_invert(P);
+#pragma unroll 1
+    for (int j = nb - 1; j >= 0; --j) {
+      const CombRec r = rec_load(recs, j);
+      const fe zi = fe_mul(inv, r.P);
+      inv = fe_mul(inv, r.Z);
+      u32 yw[8], xw[8];
+      fe_to_words(fe_mul(r.Y, zi), yw);
+      fe_to_words(fe_mul(r.X, zi), xw);
+      u32 diff = 0, xor_ = 0;
+      _Pragma("unroll") for (int q = 0; q < 8; ++q) { diff |= yw[q] ^ r.yr[q]; xor_ |= xw[q]; }
+      const bool sign_ok = xor_ == 0 || (xw[0] & 1) == ((r.meta >> 1) & 1);
+      const bool v = (r.meta & 1) && diff == 0 && sign_ok;
+      const uint64_t b0 = c0 + (uint64_t)j * stride;
+      const uint64_t ballot = __ballot(v);
+      if ((threadIdx.x & 63) == 0 && b0 + (threadIdx.x & ~63u) < a.n) a.out_bits[(b0 + threadIdx.x) >> 6] = ballot;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- committee latency
+// Latency form of the comb path for small batches (a certificate's votes, BASELINE cfg 1): one
+// equation per 128-thread block.  Wave 0 sums the 64 comb entries of sB + k(-A) with one entry per
+// lane and a 6-level butterfly (every lane ends with the sum); wave 1 decompresses R meanwhile.
+// The critical path is one square root (~31k dependent VALU instructions) instead of a lane's whole
+// verification.  Verdict: R decodes, R' == R projectively, plus the same s / key / small-order flags
+// as k_verify_comb.  Bits are OR-ed into out_bits (zeroed by the caller).
+__device__ __forceinline__ i32 digit256_at(const u32 d[8], int w) {
+  u32 word = d[0];
+  _Pragma("unroll") for (int q = 1; q < 8; ++q) word = (q == (w >> 2)) ? d[q] : word;
+  return (i32)((word >> (8 * (w & 3))) & 255u) - 128;
+}
+__device__ __forceinline__ ge_p3 shfl_xor_p3(const ge_p3& p, int mask) {
+  ge_p3 r;
+  const i32* src = reinterpret_cast<const i32*>(&p);
+  i32* dst = reinterpret_cast<i32*>(&r);
+  _Pragma("unroll") for (int q = 0; q < 40; ++q) dst[q] = __shfl_xor(src[q], mask, 64);
+  return r;
+}
+
+__global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs ca) {
+  __shared__ fe sh_rx, sh_ry;
+  __shared__ int sh_rok;
+  const uint64_t i = blockIdx.x;
+  if (i >= a.n) return;   // block-uniform
+  const Committee& cm = a.committee;
+  u32 mw[8], aw[8], sgw[16];
+  load_inputs(a, i, mw, aw, sgw);
+  const int lane = threadIdx.x & 63;
+  const int key = committee_lookup(cm, aw);
+  const int kk = key < 0 ? 0 : key;
+  u32 rw[8], sw[8];
+  _Pragma("unroll") for (int q = 0; q < 8; ++q) { rw[q] = sgw[q]; sw[q] = sgw[8 + q]; }
+  ge_p3 sum;
+  if (threadIdx.x >= 64) {
+    // wave 1: R (dalek decompression), its small-order flag
+    ge_p3 R[1];
+    u32 yc[1][8];
+    bool ok[1];
+    const u32* const wp[1] = {rw};
+    ge_decompressN<1>(R, wp, yc, ok);
+    if (lane == 0) {
+      sh_rx = R[0].X;
+      sh_ry = R[0].Y;
+      sh_rok = ok[0] && !(a.strict && ycanon_is_small_order(yc[0]));
+    }
+  } else {
+    u32 kw[8], sd[8], kd[8];
+    challenge(rw, aw, mw, kw);
+    sc_recode_radix256(sw, sd);
+    sc_recode_radix256(kw, kd);
+    const int w = lane & 31;
+    const bool bside = lane < 32;
+    const i32 d = digit256_at(bside ? sd : kd, w);
+    const ge_niels e = comb_load(bside ? ca.comb_base : cm.comb + (size_t)kk * COMB_PER_KEY, w, d);
+    sum = ge_p1p1_to_p3(ge_niels_to_p1p1(ge_niels_cneg(e, d < 0)));
+#pragma unroll 1
+    for (int m = 1; m < 64; m <<= 1) {
+      const ge_p3 o = shfl_xor_p3(sum, m);
+      sum = ge_p1p1_to_p3(ge_add_cached(sum, ge_p3_to_cached(o)));
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const u32 fl = cm.flags[kk];
+    const bool flags_ok = key >= 0 && sc_lt_l(sw) && (fl & 1) && !(a.strict && ((fl >> 1) & 1)) && sh_rok;
+    const bool eq = fe_is_zero(fe_sub(sum.X, fe_mul(sh_rx, sum.Z))) && fe_is_zero(fe_sub(sum.Y, fe_mul(sh_ry, sum.Z)));
+    if (key < 0) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;
+    if (flags_ok && eq) atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));
   }
 }
 

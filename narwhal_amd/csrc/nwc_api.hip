@@ -8,6 +8,7 @@
 // device; nothing here ever falls back to a CPU path -- a device failure is
 // an error code (< 0), never a verdict.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <atomic>
 #include <cstdarg>
 #include <cstdlib>
@@ -52,6 +53,10 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   nwc::ge_niels* base_table = nullptr;
   nwc::ge_niels_pad* base16 = nullptr;   // radix-2^16 basepoint tables (8.4 MB)
+  nwc::ge_niels_pad* comb_base = nullptr;   // basepoint comb (528 KB) for k_verify_comb
+  int comb_blocks_per_cu = 1;
+  uint32_t* uc_list = nullptr;     // k_verify_comb: equations whose key is not cached
+  uint32_t* uc_count = nullptr;
   // k_verify per-lane table slots; reused by every launch, so launches that use it are
   // serialised across streams with `scratch_free` (recorded after each such launch).
   uint8_t* scratch = nullptr;
@@ -64,12 +69,22 @@ struct DevCtx {
   nwc::u32* cm_keys = nullptr;
   nwc::u32* cm_flags = nullptr;
   nwc::ge_niels* cm_tables = nullptr;
+  nwc::ge_niels_pad* cm_comb = nullptr;   // per-key combs (committees of <= COMB_MAX_KEYS keys)
   int32_t* cm_slots = nullptr;
   uint32_t cm_n = 0, cm_slot_mask = 0;
   uint8_t* arena = nullptr;
   size_t arena_cap = 0;
+  uint8_t* pinned = nullptr;   // host staging for small calls: one H2D and one D2H per call
+  size_t pinned_cap = 0;
   std::mutex mu;
 
+  int ensure_pinned(size_t bytes) {
+    if (bytes <= pinned_cap) return 0;
+    if (pinned) { (void)hipHostFree(pinned); pinned = nullptr; pinned_cap = 0; }
+    HIP_TRY(hipHostMalloc(&pinned, bytes, hipHostMallocDefault));
+    pinned_cap = bytes;
+    return 0;
+  }
   int ensure_arena(size_t bytes) {
     if (bytes <= arena_cap) return 0;
     if (arena) { (void)hipFree(arena); arena = nullptr; arena_cap = 0; }
@@ -79,6 +94,19 @@ struct DevCtx {
     return 0;
   }
 };
+
+// committees up to this size get per-key combs (528 KB each); larger ones use the cached ladder
+#ifndef NWC_COMB_MAX_KEYS
+#define NWC_COMB_MAX_KEYS 4096
+#endif
+
+// batches up to this size take the latency kernel (k_verify_comb_wide) on the comb path
+#ifndef NWC_PINNED_STAGE_MAX
+#define NWC_PINNED_STAGE_MAX (1u << 20)
+#endif
+#ifndef NWC_WIDE_MAX
+#define NWC_WIDE_MAX 1024
+#endif
 
 std::mutex g_mu;
 std::vector<std::unique_ptr<DevCtx>> g_devs;
@@ -104,6 +132,14 @@ int init_device(DevCtx& d) {
   int bpc = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify<true, false>), 256, 0));
   d.verify_blocks_per_cu = bpc > 0 ? bpc : 1;
+  bpc = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify_comb), 256, 0));
+  d.comb_blocks_per_cu = bpc > 0 ? bpc : 1;
+  HIP_TRY(hipMalloc(&d.uc_count, sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&d.comb_base, nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad)));
+  hipLaunchKernelGGL(nwc::k_build_comb, dim3((unsigned)((nwc::COMB_PER_KEY + 255) / 256)), dim3(256), 0, d.stream,
+                     (const nwc::u32*)nullptr, 1u, d.comb_base);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipMalloc(&d.base_table, 2 * 129 * sizeof(nwc::ge_niels)));
   HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
   hipLaunchKernelGGL(nwc::k_build_base_table, dim3(5), dim3(64), 0, d.stream, d.base_table);
@@ -127,57 +163,98 @@ int require_init() {
 }
 
 // ---- launch helpers (caller holds the device mutex and has set the device) -----------------
-// Verification path: half-size equations with full-length fallback (default), or the
-// full-length ladder for every lane (NWC_VERIFY_PATH=full; used to cross-check the two paths).
-bool half_path() {
-  static const bool half = [] {
+// Verification path (NWC_VERIFY_PATH): default = the doubling-free comb kernel for equations whose
+// key is in the committee cache (when the committee has combs) and half-size equations with
+// full-length fallback for the rest; "half" = no comb kernel; "full" = the full-length ladder for
+// every lane.  The alternatives exist to cross-check the paths against each other.
+enum class VPath { Default, Half, Full };
+VPath verify_path() {
+  static const VPath p = [] {
     const char* e = std::getenv("NWC_VERIFY_PATH");
-    return !(e && std::strcmp(e, "full") == 0);
+    if (e && std::strcmp(e, "full") == 0) return VPath::Full;
+    if (e && std::strcmp(e, "half") == 0) return VPath::Half;
+    return VPath::Default;
   }();
-  return half;
+  return p;
+}
+
+int ensure_scratch(DevCtx& d, size_t bytes, uint64_t n) {
+  if (bytes <= d.scratch_cap && n <= d.fb_cap) return 0;
+  HIP_TRY(hipEventSynchronize(d.scratch_free));
+  if (bytes > d.scratch_cap) {
+    if (d.scratch) HIP_TRY(hipFree(d.scratch));
+    d.scratch = nullptr;
+    d.scratch_cap = 0;
+    HIP_TRY(hipMalloc(&d.scratch, bytes));
+    d.scratch_cap = bytes;
+  }
+  if (n > d.fb_cap) {
+    if (d.fb_list) HIP_TRY(hipFree(d.fb_list));
+    if (d.uc_list) HIP_TRY(hipFree(d.uc_list));
+    d.fb_list = nullptr;
+    d.uc_list = nullptr;
+    d.fb_cap = 0;
+    const size_t c = n + n / 2 + 4096;
+    HIP_TRY(hipMalloc(&d.fb_list, 4 * c));
+    HIP_TRY(hipMalloc(&d.uc_list, 4 * c));
+    d.fb_cap = c;
+  }
+  return 0;
 }
 
 int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
                   hipStream_t s) {
   if (n == 0) return 0;
+  const VPath path = verify_path();
+  const bool comb = path == VPath::Default && d.cm_n && d.cm_comb;
   const uint64_t tiles = (n + 255) / 256;
   // persistent grid: a few blocks per resident slot so the tail is short
   const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * 4;
   const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
-  const size_t per_lane = 2 * nwc::TAB_BYTES_PER_LANE;
-  if ((size_t)grid * 256 * per_lane > d.scratch_cap || n > d.fb_cap) {
-    HIP_TRY(hipEventSynchronize(d.scratch_free));
-    if ((size_t)grid * 256 * per_lane > d.scratch_cap) {
-      if (d.scratch) HIP_TRY(hipFree(d.scratch));
-      d.scratch = nullptr;
-      d.scratch_cap = 0;
-      const size_t full = (size_t)cap * 256 * per_lane;
-      HIP_TRY(hipMalloc(&d.scratch, full));
-      d.scratch_cap = full;
-    }
-    if (n > d.fb_cap) {
-      if (d.fb_list) HIP_TRY(hipFree(d.fb_list));
-      d.fb_list = nullptr;
-      d.fb_cap = 0;
-      const size_t c = n + n / 2 + 4096;
-      HIP_TRY(hipMalloc(&d.fb_list, 4 * c));
-      d.fb_cap = c;
-    }
+  size_t need = (size_t)cap * 256 * 2 * nwc::TAB_BYTES_PER_LANE;
+  // comb grid: resident blocks only, sized so every lane runs the same number of COMB_BATCH chunks
+  unsigned gridc = 0;
+  if (comb) {
+    const uint64_t resident = (uint64_t)d.cus * d.comb_blocks_per_cu;
+    const uint64_t chunks = (tiles + resident * nwc::COMB_BATCH - 1) / (resident * nwc::COMB_BATCH);
+    gridc = (unsigned)((tiles + chunks * nwc::COMB_BATCH - 1) / (chunks * nwc::COMB_BATCH));
+    need = std::max(need, (size_t)resident * 256 * nwc::COMB_BYTES_PER_LANE);
   }
+  if (int rc = ensure_scratch(d, need, n)) return rc;
   HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
   static const uint32_t force_every = [] {
     const char* e = std::getenv("NWC_FORCE_FALLBACK_EVERY");
     return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
   }();
-  const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_slots, d.cm_slot_mask, d.cm_n};
+  const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
   nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base16, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
-  const bool half = half_path();
+  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base};
+  const bool half = path != VPath::Full;
   if (half) HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
-  if (half && cm.n) hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a);
-  else if (half) hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((nwc::k_verify<false, false>), dim3(grid), dim3(256), 0, s, a);
+  if (comb) {
+    HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
+    if (n <= NWC_WIDE_MAX) {
+      // small batches: one block per equation, critical path = one square root
+      HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
+      hipLaunchKernelGGL(nwc::k_verify_comb_wide, dim3((unsigned)n), dim3(128), 0, s, a, ca);
+    } else {
+      hipLaunchKernelGGL(nwc::k_verify_comb, dim3(gridc), dim3(256), 0, s, a, ca);
+    }
+    HIP_TRY(hipGetLastError());
+    // uncached keys: half-size equations in list mode (blocks exit at once when the list is empty)
+    nwc::VerifyArgs l = a;
+    l.committee.n = 0;
+    const unsigned lgrid = (unsigned)std::min<uint64_t>(grid, (uint64_t)d.cus * d.verify_blocks_per_cu);
+    hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3(lgrid), dim3(256), 0, s, l, ca);
+  } else if (half && cm.n) {
+    hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a, ca);
+  } else if (half) {
+    hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a, ca);
+  } else {
+    hipLaunchKernelGGL((nwc::k_verify<false, false>), dim3(grid), dim3(256), 0, s, a, ca);
+  }
   HIP_TRY(hipGetLastError());
   if (half) {
     // lanes whose reduction failed are rare (|c| or d >= 2^147); a few blocks suffice
@@ -269,6 +346,21 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
   uint8_t* dp = c.take<uint8_t>(32 * n);
   uint8_t* ds = c.take<uint8_t>(64 * n);
   uint64_t* dout = c.take<uint64_t>(8 * words);
+  if (need <= NWC_PINNED_STAGE_MAX) {
+    // small call (a certificate, a header): pack into pinned memory, one H2D, one D2H
+    if (int rc = d.ensure_pinned(NWC_PINNED_STAGE_MAX)) return rc;
+    uint8_t* h = d.pinned;
+    std::memcpy(h + (dm - d.arena), msg_index ? msgs : msgs + (msg_stride ? 32 * lo : 0), msg_bytes);
+    if (msg_index) std::memcpy(h + ((uint8_t*)dmi - d.arena), msg_index + lo, 4 * n);
+    std::memcpy(h + (dp - d.arena), pks + 32 * lo, 32 * n);
+    std::memcpy(h + (ds - d.arena), sigs + 64 * lo, 64 * n);
+    HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena), hipMemcpyHostToDevice, d.stream));
+    if (int rc = launch_verify(d, dm, dmi, msg_stride ? 1 : 0, dp, ds, n, strict, dout, d.stream)) return rc;
+    HIP_TRY(hipMemcpyAsync(h, dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    std::memcpy(out_words.data(), h, 8 * words);
+    return 0;
+  }
   if (msg_index) {
     HIP_TRY(hipMemcpyAsync(dm, msgs, msg_bytes, hipMemcpyHostToDevice, d.stream));
     HIP_TRY(hipMemcpyAsync(dmi, msg_index + lo, 4 * n, hipMemcpyHostToDevice, d.stream));
@@ -324,6 +416,11 @@ void nwc_shutdown(void) {
     if (d->cm_flags) (void)hipFree(d->cm_flags);
     if (d->cm_tables) (void)hipFree(d->cm_tables);
     if (d->cm_slots) (void)hipFree(d->cm_slots);
+    if (d->cm_comb) (void)hipFree(d->cm_comb);
+    if (d->comb_base) (void)hipFree(d->comb_base);
+    if (d->pinned) (void)hipHostFree(d->pinned);
+    if (d->uc_list) (void)hipFree(d->uc_list);
+    if (d->uc_count) (void)hipFree(d->uc_count);
     if (d->scratch_free) (void)hipEventDestroy(d->scratch_free);
     if (d->base_table) (void)hipFree(d->base_table);
     if (d->base16) (void)hipFree(d->base16);
@@ -460,7 +557,8 @@ int nwc_set_committee(const uint8_t* pks, size_t n) {
     if (d.cm_flags) HIP_TRY(hipFree(d.cm_flags));
     if (d.cm_tables) HIP_TRY(hipFree(d.cm_tables));
     if (d.cm_slots) HIP_TRY(hipFree(d.cm_slots));
-    d.cm_keys = nullptr; d.cm_flags = nullptr; d.cm_tables = nullptr; d.cm_slots = nullptr;
+    if (d.cm_comb) HIP_TRY(hipFree(d.cm_comb));
+    d.cm_keys = nullptr; d.cm_flags = nullptr; d.cm_tables = nullptr; d.cm_slots = nullptr; d.cm_comb = nullptr;
     d.cm_n = 0; d.cm_slot_mask = 0;
     if (n == 0) continue;
     HIP_TRY(hipMalloc(&d.cm_keys, 32 * n));
@@ -473,6 +571,14 @@ int nwc_set_committee(const uint8_t* pks, size_t n) {
     hipLaunchKernelGGL(nwc::k_build_key_tables, dim3(grid), dim3(256), 0, d.stream, d.cm_keys, (nwc::u32)n,
                        d.cm_tables, d.cm_flags);
     HIP_TRY(hipGetLastError());
+    if (n <= NWC_COMB_MAX_KEYS) {
+      // per-key combs for the doubling-free path (528 KB per key)
+      const size_t entries = n * nwc::COMB_PER_KEY;
+      HIP_TRY(hipMalloc(&d.cm_comb, entries * sizeof(nwc::ge_niels_pad)));
+      hipLaunchKernelGGL(nwc::k_build_comb, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, d.stream,
+                         d.cm_keys, (nwc::u32)n, d.cm_comb);
+      HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipStreamSynchronize(d.stream));
     d.cm_n = (uint32_t)n;
     d.cm_slot_mask = slots - 1;
