@@ -73,6 +73,40 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
  * depend on it. */
 int nwc_set_committee(const uint8_t* pks, size_t n);
 
+/* ---- primary messages ---------------------------------------- */
+/* config::Committee for the message checks (config/src/lib.rs:134-212): n authorities with
+ * their keys, stakes (Committee::stake) and worker ids (Committee::worker): authority k runs
+ * workers worker_ids[worker_offsets[k] .. worker_offsets[k+1]).  Also sets the key cache
+ * (nwc_set_committee); a later nwc_set_committee drops the stake/worker tables. */
+int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t n,
+                             const uint32_t* worker_offsets, const uint32_t* worker_ids);
+
+/* DagError codes of nwc_sanitize_messages (primary/src/error.rs) */
+#define NWC_DAG_OK 0
+#define NWC_DAG_INVALID_SIGNATURE 1
+#define NWC_DAG_INVALID_HEADER_ID 2
+#define NWC_DAG_MALFORMED_HEADER 3
+#define NWC_DAG_UNKNOWN_AUTHORITY 4
+#define NWC_DAG_AUTHORITY_REUSE 5
+#define NWC_DAG_CERTIFICATE_REQUIRES_QUORUM 6
+#define NWC_DAG_TOO_OLD 7
+#define NWC_DAG_SERIALIZATION_ERROR 8
+#define NWC_DAG_UNEXPECTED_VOTE 9
+#define NWC_DAG_UNEXPECTED_MESSAGE 10
+
+/* Core::sanitize_header / sanitize_vote / sanitize_certificate (primary/src/core.rs:306-346)
+ * for a batch of wire messages, each the bincode bytes of a PrimaryMessage as received by
+ * PrimaryReceiverHandler::dispatch (primary/src/primary.rs:224-240): message i is
+ * data[offsets[i] .. offsets[i+1]).  Decoding (incl. the base64 PublicKeys), Header::digest,
+ * Vote::digest, Certificate::digest, the committee checks of Header::verify / Vote::verify /
+ * Certificate::verify (primary/src/messages.rs:48-67, 131-142, 189-215) and every signature run
+ * on the GPU.  gc_round: TooOld for headers and certificates (0 disables).  vote_target
+ * (nullable, 72 B = id || round u64 LE || origin): the current header of sanitize_vote.
+ * codes[i] = NWC_DAG_*; digests32 (nullable): the message's digest; kinds (nullable):
+ * 0 header, 1 vote, 2 certificate, 3 other.  Needs nwc_set_committee_config. */
+int nwc_sanitize_messages(const uint8_t* data, const uint64_t* offsets, size_t m, uint64_t gc_round,
+                          const uint8_t* vote_target, int32_t* codes, uint8_t* digests32, uint8_t* kinds);
+
 /* ---- digests -------------------------------------------------------------------------- */
 /* Sha512::digest(bytes)[..32] -- worker/src/processor.rs:38 and crypto's `Hash for &[u8]`
  * (crypto/src/tests/crypto_tests.rs:8-12). */

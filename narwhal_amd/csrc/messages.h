@@ -1,0 +1,424 @@
+// Primary messages on the GPU: bincode/base64 ingestion, message digests and the structural
+// checks of Header::verify / Vote::verify / Certificate::verify.
+//
+//   k_parse_messages     one lane per serialized PrimaryMessage (bincode 1.3 legacy config:
+//                        little-endian fixint, u64 lengths; primary/src/primary.rs:230):
+//                        decodes the message, the base64 PublicKey strings
+//                        (crypto/src/lib.rs:94-112), computes Header::digest
+//                        (primary/src/messages.rs:70-84), Vote::digest (:145-153) and
+//                        Certificate::digest (:226-234), applies the committee checks in the
+//                        reference's order, and emits the signature equations: one strict
+//                        equation per message (the header's or the vote's signature) and one
+//                        batch-leaf equation per certificate vote.
+//   k_finalize_messages  combines the structural code with the equation verdicts into the
+//                        DagError the reference returns (primary/src/error.rs).
+//
+// Wire layout (bincode of PrimaryMessage, primary/src/primary.rs:33-38):
+//   u32 variant (0 Header, 1 Vote, 2 Certificate, 3 CertificatesRequest)
+//   Header      = str author, u64 round, u64 P, P x (32-B digest, u32 worker id), u64 Q,
+//                 Q x 32-B digest, 32-B id, 64-B signature
+//   Vote        = 32-B id, u64 round, str origin, str author, 64-B signature
+//   Certificate = Header, u64 V, V x (str key, 64-B signature)
+//   str         = u64 length, bytes: a PublicKey is the standard base64 of its 32 bytes.
+// Decoding subset: a key string is accepted iff it is the canonical padded standard base64 of 32
+// bytes (44 characters, the 2 trailing bits of the last symbol zero) -- what every honest node
+// sends (base64::encode).  base64 0.13 may accept other forms (unpadded strings, longer strings
+// whose first 32 decoded bytes are used); those are reported as SerializationError here
+// (parity unpinned).  Trailing bytes after a message are ignored, as bincode's
+// legacy config does.
+#pragma once
+#include <stdint.h>
+
+namespace nwc {
+
+enum DagCode : u32 {
+  DAG_OK = 0,
+  DAG_INVALID_SIGNATURE = 1,      // DagError::InvalidSignature
+  DAG_INVALID_HEADER_ID = 2,      // DagError::InvalidHeaderId
+  DAG_MALFORMED_HEADER = 3,       // DagError::MalformedHeader
+  DAG_UNKNOWN_AUTHORITY = 4,      // DagError::UnknownAuthority
+  DAG_AUTHORITY_REUSE = 5,        // DagError::AuthorityReuse
+  DAG_REQUIRES_QUORUM = 6,        // DagError::CertificateRequiresQuorum
+  DAG_TOO_OLD = 7,                // DagError::TooOld
+  DAG_SERIALIZATION = 8,          // DagError::SerializationError
+  DAG_UNEXPECTED_VOTE = 9,        // DagError::UnexpectedVote
+  DAG_UNEXPECTED_MESSAGE = 10,    // CertificatesRequest (not a Core message)
+};
+enum MsgKind : u32 { MSG_HEADER = 0, MSG_VOTE = 1, MSG_CERTIFICATE = 2, MSG_OTHER = 3 };
+
+// Stake / worker tables of config::Committee (config/src/lib.rs:134-212), device resident.
+struct CommitteeCfg {
+  const uint64_t* stakes;      // per committee index (Committee::stake; 0 = no voting rights)
+  const uint32_t* worker_off;  // n + 1
+  const uint32_t* worker_ids;  // worker ids of authority k: [worker_off[k], worker_off[k+1])
+  uint64_t quorum;             // 2 * total / 3 + 1 (Committee::quorum_threshold)
+  uint32_t n;
+};
+
+// Core::sanitize_vote's expectation (the current header), optional
+struct VoteTarget { u32 id[8]; u32 origin[8]; uint64_t round; int enabled; };
+
+struct MsgArgs {
+  const uint8_t* data;          // messages, 4-byte aligned base, >= 8 bytes of padding at the end
+  const uint64_t* offsets;      // m + 1
+  uint64_t m;
+  uint64_t gc_round;            // Core::gc_round (TooOld for headers and certificates)
+  VoteTarget target;
+  uint8_t* hashbuf;             // per-message scratch for the header digest input
+  // strict equations: one per message
+  uint8_t* eq_msg;              // m x 32
+  uint8_t* eq_pk;               // m x 32
+  uint8_t* eq_sig;              // m x 64
+  // batch-leaf equations: the certificates' votes
+  uint8_t* v_pk;                // cap x 32
+  uint8_t* v_sig;               // cap x 64
+  uint32_t* v_msg;              // cap: equation -> message index (its certificate digest)
+  uint8_t* cdig;                // m x 32: Certificate::digest per message (votes sign it)
+  uint32_t* v_total;            // atomic vote-slot allocator
+  uint64_t v_cap;
+  uint32_t* used;               // m x used_words: AuthorityReuse bitmaps
+  uint32_t used_words;
+  uint32_t* rec;                // m x 4: kind, pre code, post code, vote base
+  uint32_t* rec_n;              // m: vote count
+  uint8_t* digests;             // m x 32: the message's digest (Header::digest / Vote::digest /
+                                //         Certificate::digest), for the caller
+};
+
+// ---- byte access: aligned dword loads + alignbyte (the data base is 4-byte aligned) --------
+template <int K>
+__device__ __forceinline__ void ld_words(const uint8_t* base, uint64_t off, u32 out[K]) {
+  const u32* q = reinterpret_cast<const u32*>(base + (off & ~(uint64_t)3));
+  const u32 sh = (u32)(off & 3);
+  u32 w[K + 1];
+  _Pragma("unroll") for (int i = 0; i <= K; ++i) w[i] = q[i];
+  _Pragma("unroll") for (int i = 0; i < K; ++i) out[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+}
+__device__ __forceinline__ uint64_t ld_u64(const uint8_t* base, uint64_t off) {
+  u32 w[2];
+  ld_words<2>(base, off, w);
+  return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+}
+__device__ __forceinline__ u32 ld_u32(const uint8_t* base, uint64_t off) {
+  u32 w[1];
+  ld_words<1>(base, off, w);
+  return w[0];
+}
+
+// standard base64 symbol value, or -1
+__device__ __forceinline__ i32 b64_val(u32 c) {
+  i32 v = -1;
+  v = (c >= 'A' && c <= 'Z') ? (i32)c - 'A' : v;
+  v = (c >= 'a' && c <= 'z') ? (i32)c - 'a' + 26 : v;
+  v = (c >= '0' && c <= '9') ? (i32)c - '0' + 52 : v;
+  v = (c == '+') ? 62 : v;
+  v = (c == '/') ? 63 : v;
+  return v;
+}
+// 44 characters (11 words) -> 32 bytes; false unless canonical padded standard base64
+__device__ __forceinline__ bool b64_decode32(const u32 s[11], u32 out[8]) {
+  bool ok = true;
+  u32 bits = 0;   // 24-bit group
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) out[i] = 0;
+  _Pragma("unroll") for (int g = 0; g < 11; ++g) {
+    const u32 word = s[g];
+    bits = 0;
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) {
+      const u32 c = (word >> (8 * k)) & 255u;
+      const int pos = 4 * g + k;
+      if (pos == 43) {
+        ok = ok && (c == '=');
+        bits <<= 6;
+      } else {
+        const i32 v = b64_val(c);
+        ok = ok && (v >= 0);
+        bits = (bits << 6) | (u32)(v & 63);
+      }
+    }
+    // group g gives bytes 3g .. 3g+2 (the last group only 2: bytes 30, 31; its low 8 bits are the
+    // 2 trailing bits of symbol 42 plus the padding and must be zero)
+    _Pragma("unroll") for (int b = 0; b < 3; ++b) {
+      const int byte = 3 * g + b;
+      const u32 val = (bits >> (16 - 8 * b)) & 255u;
+      if (byte < 32) out[byte >> 2] |= val << (8 * (byte & 3));
+    }
+    if (g == 10) ok = ok && ((bits & 255u) == 0);
+  }
+  return ok;
+}
+
+// SHA-512[..32] of a 16-byte-aligned buffer (little-endian digest words)
+__device__ void sha512_trunc32_buf(const uint8_t* p, uint64_t len, u32 out[8]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint64_t full = len >> 7;
+  const uint64_t total = (len + 17 + 127) >> 7;
+  uint64_t st[8];
+  sha512_init_state(st);
+#pragma unroll 1
+  for (uint64_t b = 0; b < total; ++b) {
+    uint64_t w[16];
+    if (b < full) {
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) {
+        const uint4 v = q[8 * b + j];
+        w[2 * j] = be64_from_le32(v.x, v.y);
+        w[2 * j + 1] = be64_from_le32(v.z, v.w);
+      }
+    } else {
+      const ShaBlock r = sha_block_bytes(p, len, b);
+      _Pragma("unroll") for (int j = 0; j < 16; ++j) w[j] = r.w[j];
+    }
+    sha512_compress(st, w);
+  }
+  _Pragma("unroll") for (int j = 0; j < 4; ++j) {
+    out[2 * j] = __builtin_bswap32((u32)(st[j] >> 32));
+    out[2 * j + 1] = __builtin_bswap32((u32)st[j]);
+  }
+}
+
+// SHA-512[..32] of id(32) || round(8, LE) || key(32): Vote::digest, Certificate::digest
+__device__ __forceinline__ void digest72(const u32 id[8], uint64_t round, const u32 key[8], u32 out[8]) {
+  u32 wds[18];
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) { wds[i] = id[i]; wds[10 + i] = key[i]; }
+  wds[8] = (u32)round;
+  wds[9] = (u32)(round >> 32);
+  u32 dg[16];
+  sha512_one_block(wds, 72, dg);
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) out[i] = dg[i];
+}
+
+__device__ __forceinline__ void st_words(uint8_t* dst, const u32* w, int k) {
+  u32* d = reinterpret_cast<u32*>(dst);
+  for (int i = 0; i < k; ++i) d[i] = w[i];
+}
+
+struct MsgReader {
+  const uint8_t* base;
+  uint64_t pos, end;
+  bool ok;
+  __device__ __forceinline__ bool need(uint64_t n) {
+    ok = ok && pos <= end && n <= end - pos;
+    return ok;
+  }
+  __device__ __forceinline__ uint64_t u64() {
+    if (!need(8)) return 0;
+    const uint64_t v = ld_u64(base, pos);
+    pos += 8;
+    return v;
+  }
+  __device__ __forceinline__ void bytes32(u32 out[8]) {
+    if (!need(32)) { for (int i = 0; i < 8; ++i) out[i] = 0; return; }
+    ld_words<8>(base, pos, out);
+    pos += 32;
+  }
+  __device__ __forceinline__ void bytes64(u32 out[16]) {
+    if (!need(64)) { for (int i = 0; i < 16; ++i) out[i] = 0; return; }
+    ld_words<16>(base, pos, out);
+    pos += 64;
+  }
+  // a PublicKey: u64 length 44 + canonical base64
+  __device__ __forceinline__ void key(u32 out[8]) {
+    const uint64_t len = u64();
+    ok = ok && len == 44;
+    if (!need(44)) { for (int i = 0; i < 8; ++i) out[i] = 0; return; }
+    u32 s[11];
+    ld_words<11>(base, pos, s);
+    pos += 44;
+    ok = b64_decode32(s, out) && ok;
+  }
+};
+
+__device__ __forceinline__ bool words_eq8(const u32 a[8], const u32 b[8]) {
+  u32 d = 0;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) d |= a[i] ^ b[i];
+  return d == 0;
+}
+__device__ __forceinline__ uint64_t member_stake(const CommitteeCfg& cc, int idx) {
+  return idx >= 0 ? cc.stakes[idx] : 0;
+}
+
+// Header fields shared by Header and Certificate messages (reader positioned at the header).
+struct HeaderView {
+  u32 author[8], id[8], sig[16], digest[8];
+  uint64_t round;
+  int aidx;            // committee index of the author (-1: not a member)
+  bool worker_bad;     // a payload worker id the author does not run (MalformedHeader)
+};
+__device__ void parse_header(MsgReader& r, const Committee& cm, const CommitteeCfg& cc, uint8_t* hb, HeaderView& h) {
+  r.key(h.author);
+  const uint64_t round_off = r.pos;
+  h.round = r.u64();
+  const uint64_t P = r.u64();
+  r.need(P <= (1ull << 40) ? P * 36 : ~0ull);
+  const uint64_t pay_off = r.pos;
+  if (r.ok) r.pos += P * 36;
+  const uint64_t Q = r.u64();
+  r.need(Q <= (1ull << 40) ? Q * 32 : ~0ull);
+  const uint64_t par_off = r.pos;
+  if (r.ok) r.pos += Q * 32;
+  r.bytes32(h.id);
+  r.bytes64(h.sig);
+  h.aidx = r.ok ? committee_lookup(cm, h.author) : -1;
+  h.worker_bad = false;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) h.digest[i] = 0;
+  if (!r.ok) return;
+  // worker ids (Committee::worker(author, id)); only consulted when the author is a member
+  if (h.aidx >= 0) {
+    const uint32_t w0 = cc.worker_off[h.aidx], w1 = cc.worker_off[h.aidx + 1];
+    for (uint64_t e = 0; e < P; ++e) {
+      const u32 wid = ld_u32(r.base, pay_off + 36 * e + 32);
+      bool found = false;
+      for (uint32_t k = w0; k < w1; ++k) found = found || (cc.worker_ids[k] == wid);
+      h.worker_bad = h.worker_bad || !found;
+    }
+  }
+  // Header::digest input: author(32) || round(8) || payload entries (36 each) || parents (32 each),
+  // gathered into the 128-B-aligned scratch hb (every destination offset is a multiple of 4)
+  u32* d = reinterpret_cast<u32*>(hb);
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) d[i] = h.author[i];
+  d[8] = (u32)h.round;
+  d[9] = (u32)(h.round >> 32);
+  (void)round_off;
+  const uint64_t pw = P * 9, qw = Q * 8;
+  for (uint64_t k = 0; k < pw; ++k) d[10 + k] = ld_u32(r.base, pay_off + 4 * k);
+  for (uint64_t k = 0; k < qw; ++k) d[10 + pw + k] = ld_u32(r.base, par_off + 4 * k);
+  sha512_trunc32_buf(hb, 40 + 36 * P + 32 * Q, h.digest);
+}
+
+__global__ __launch_bounds__(256) void k_parse_messages(MsgArgs a, Committee cm, CommitteeCfg cc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m) return;
+  MsgReader r{a.data, a.offsets[i], a.offsets[i + 1], true};
+  const uint64_t variant = ld_u32(a.data, r.pos);
+  r.need(4);
+  r.pos += 4;
+  u32 kind = variant <= 2 ? (u32)variant : (u32)MSG_OTHER;
+  if (!r.ok) kind = MSG_OTHER;
+  u32 pre = DAG_OK, post = DAG_OK, vbase = 0, vcount = 0;
+  u32 eq_msg[8], eq_pk[8], eq_sig[16], dig[8], cd[8];
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) { eq_msg[k] = 0; eq_pk[k] = 0; dig[k] = 0; cd[k] = 0; }
+  _Pragma("unroll") for (int k = 0; k < 16; ++k) eq_sig[k] = 0;
+  uint8_t* hb = a.hashbuf + ((a.offsets[i] + 127) & ~(uint64_t)127) + 128 * i;
+  if (kind == MSG_HEADER || kind == MSG_CERTIFICATE) {
+    HeaderView h;
+    parse_header(r, cm, cc, hb, h);
+    // Certificate: votes
+    uint64_t V = 0;
+    bool reuse_first = false, unknown_first = false;
+    uint64_t weight = 0;
+    if (kind == MSG_CERTIFICATE) {
+      V = r.u64();
+      r.need(V <= (1ull << 32) ? V * 116 : ~0ull);   // >= 116 bytes per vote
+      if (r.ok) {
+        vbase = atomicAdd(a.v_total, (uint32_t)V);
+        if ((uint64_t)vbase + V > a.v_cap) { r.ok = false; vbase = 0; }
+      }
+      digest72(h.id, h.round, h.author, cd);
+      uint32_t* used = a.used + i * a.used_words;
+      for (u32 k = 0; k < a.used_words; ++k) used[k] = 0;
+      bool vote_err = false;
+      for (uint64_t v = 0; v < V && r.ok; ++v) {
+        u32 key[8], sg[16];
+        r.key(key);
+        r.bytes64(sg);
+        if (!r.ok) break;
+        st_words(a.v_pk + 32 * (vbase + v), key, 8);
+        st_words(a.v_sig + 64 * (vbase + v), sg, 16);
+        a.v_msg[vbase + v] = (uint32_t)i;
+        // Certificate::verify (primary/src/messages.rs:198-208): reuse, then stake, in vote order
+        if (!vote_err) {
+          const int kidx = committee_lookup(cm, key);
+          const uint64_t st = member_stake(cc, kidx);
+          const bool reused = kidx >= 0 && ((used[kidx >> 5] >> (kidx & 31)) & 1);
+          if (reused) { reuse_first = true; vote_err = true; }
+          else if (st == 0) { unknown_first = true; vote_err = true; }
+          else { used[kidx >> 5] |= 1u << (kidx & 31); weight += st; }
+        }
+      }
+    }
+    if (!r.ok) {
+      pre = DAG_SERIALIZATION;
+      V = 0;   // (slots of a truncated vote list keep the host's zero-filled v_msg: index 0 is valid)
+    } else if (kind == MSG_CERTIFICATE && h.round == 0 && h.aidx >= 0 &&
+               [&] { u32 z = 0; for (int k = 0; k < 8; ++k) z |= h.id[k]; return z == 0; }()) {
+      // genesis (Certificate::genesis(committee).contains(self), :190-193): id == 0, round 0,
+      // origin a committee member -- checked after TooOld (Core::sanitize_certificate)
+      pre = a.gc_round > h.round ? DAG_TOO_OLD : DAG_OK;
+      post = 0x100;   // marker: genesis, no signature checks
+    } else if (a.gc_round > h.round) {
+      pre = DAG_TOO_OLD;
+    } else if (!words_eq8(h.digest, h.id)) {
+      pre = DAG_INVALID_HEADER_ID;
+    } else if (member_stake(cc, h.aidx) == 0) {
+      pre = DAG_UNKNOWN_AUTHORITY;
+    } else if (h.worker_bad) {
+      pre = DAG_MALFORMED_HEADER;
+    }
+    if (kind == MSG_CERTIFICATE && post == DAG_OK) {
+      post = reuse_first ? DAG_AUTHORITY_REUSE : unknown_first ? DAG_UNKNOWN_AUTHORITY
+             : (weight < cc.quorum ? DAG_REQUIRES_QUORUM : DAG_OK);
+    }
+    vcount = (u32)V;
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) { eq_msg[k] = h.id[k]; eq_pk[k] = h.author[k]; }
+    _Pragma("unroll") for (int k = 0; k < 16; ++k) eq_sig[k] = h.sig[k];
+    if (kind == MSG_HEADER) { _Pragma("unroll") for (int k = 0; k < 8; ++k) dig[k] = h.digest[k]; }
+    else { _Pragma("unroll") for (int k = 0; k < 8; ++k) dig[k] = cd[k]; }
+  } else if (kind == MSG_VOTE) {
+    u32 id[8], origin[8], author[8], sg[16];
+    r.bytes32(id);
+    const uint64_t round = r.u64();
+    r.key(origin);
+    r.key(author);
+    r.bytes64(sg);
+    digest72(id, round, origin, dig);
+    if (!r.ok) {
+      pre = DAG_SERIALIZATION;
+    } else if (a.target.enabled && a.target.round > round) {
+      pre = DAG_TOO_OLD;   // Core::sanitize_vote (primary/src/core.rs:319-322)
+    } else if (a.target.enabled && !(words_eq8(id, a.target.id) && words_eq8(origin, a.target.origin) &&
+                                     round == a.target.round)) {
+      pre = DAG_UNEXPECTED_VOTE;   // core.rs:325-330
+    } else if (member_stake(cc, committee_lookup(cm, author)) == 0) {
+      pre = DAG_UNKNOWN_AUTHORITY;   // Vote::verify (messages.rs:133-136)
+    }
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) { eq_msg[k] = dig[k]; eq_pk[k] = author[k]; }
+    _Pragma("unroll") for (int k = 0; k < 16; ++k) eq_sig[k] = sg[k];
+  } else {
+    pre = r.ok && variant == 3 ? DAG_UNEXPECTED_MESSAGE : DAG_SERIALIZATION;
+  }
+  st_words(a.eq_msg + 32 * i, eq_msg, 8);
+  st_words(a.eq_pk + 32 * i, eq_pk, 8);
+  st_words(a.eq_sig + 64 * i, eq_sig, 16);
+  st_words(a.cdig + 32 * i, cd, 8);
+  if (a.digests) st_words(a.digests + 32 * i, dig, 8);
+  a.rec[4 * i + 0] = kind;
+  a.rec[4 * i + 1] = pre;
+  a.rec[4 * i + 2] = post;
+  a.rec[4 * i + 3] = vbase;
+  a.rec_n[i] = vcount;
+}
+
+// code[i] per the reference's order: pre (serialization, TooOld, id, authority, workers, vote
+// target) -> signature of the header / vote -> votes' reuse / stake / quorum -> verify_batch.
+__global__ void k_finalize_messages(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ rec_n,
+                                    const uint64_t* __restrict__ strict_bits, const uint64_t* __restrict__ leaf_bits,
+                                    uint64_t m, int32_t* __restrict__ codes) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const u32 kind = rec[4 * i], pre = rec[4 * i + 1], post = rec[4 * i + 2], vbase = rec[4 * i + 3];
+  const u32 vn = rec_n[i];
+  u32 code = pre;
+  if (code == DAG_OK && post != 0x100) {
+    const bool sig_ok = (strict_bits[i >> 6] >> (i & 63)) & 1;
+    if (!sig_ok) code = DAG_INVALID_SIGNATURE;
+    else if (kind == MSG_CERTIFICATE) {
+      if (post != DAG_OK) code = post;
+      else {
+        bool all = true;
+        for (u32 v = vbase; v < vbase + vn; ++v) all = all && ((leaf_bits[v >> 6] >> (v & 63)) & 1);
+        code = all ? DAG_OK : DAG_INVALID_SIGNATURE;
+      }
+    }
+  }
+  codes[i] = (int32_t)code;
+}
+
+}  // namespace nwc

@@ -22,6 +22,7 @@
 
 #include "nwc.h"
 #include "kernels.hip"
+#include "messages.h"
 
 namespace {
 
@@ -74,6 +75,14 @@ struct DevCtx {
   uint32_t cm_n = 0, cm_slot_mask = 0;
   uint8_t* arena = nullptr;
   size_t arena_cap = 0;
+  // config::Committee stake / worker tables (nwc_set_committee_config)
+  uint64_t* cc_stakes = nullptr;
+  uint32_t* cc_worker_off = nullptr;
+  uint32_t* cc_worker_ids = nullptr;
+  uint64_t cc_quorum = 0;
+  uint32_t cc_n = 0;
+  uint8_t* msg_arena = nullptr;   // nwc_sanitize_messages buffers
+  size_t msg_arena_cap = 0;
   uint8_t* pinned = nullptr;   // host staging for small calls: one H2D and one D2H per call
   size_t pinned_cap = 0;
   std::mutex mu;
@@ -419,6 +428,10 @@ void nwc_shutdown(void) {
     if (d->cm_comb) (void)hipFree(d->cm_comb);
     if (d->comb_base) (void)hipFree(d->comb_base);
     if (d->pinned) (void)hipHostFree(d->pinned);
+    if (d->cc_stakes) (void)hipFree(d->cc_stakes);
+    if (d->cc_worker_off) (void)hipFree(d->cc_worker_off);
+    if (d->cc_worker_ids) (void)hipFree(d->cc_worker_ids);
+    if (d->msg_arena) (void)hipFree(d->msg_arena);
     if (d->uc_list) (void)hipFree(d->uc_list);
     if (d->uc_count) (void)hipFree(d->uc_count);
     if (d->scratch_free) (void)hipEventDestroy(d->scratch_free);
@@ -559,6 +572,12 @@ int nwc_set_committee(const uint8_t* pks, size_t n) {
     if (d.cm_slots) HIP_TRY(hipFree(d.cm_slots));
     if (d.cm_comb) HIP_TRY(hipFree(d.cm_comb));
     d.cm_keys = nullptr; d.cm_flags = nullptr; d.cm_tables = nullptr; d.cm_slots = nullptr; d.cm_comb = nullptr;
+    // stake / worker tables are indexed like the cache: a new cache invalidates them
+    // (nwc_set_committee_config sets them again right after)
+    if (d.cc_stakes) HIP_TRY(hipFree(d.cc_stakes));
+    if (d.cc_worker_off) HIP_TRY(hipFree(d.cc_worker_off));
+    if (d.cc_worker_ids) HIP_TRY(hipFree(d.cc_worker_ids));
+    d.cc_stakes = nullptr; d.cc_worker_off = nullptr; d.cc_worker_ids = nullptr; d.cc_n = 0;
     d.cm_n = 0; d.cm_slot_mask = 0;
     if (n == 0) continue;
     HIP_TRY(hipMalloc(&d.cm_keys, 32 * n));
@@ -706,6 +725,141 @@ int nwc_dev_keygen_sign(const void* d_seeds, const void* d_msgs, uint64_t n, voi
   hipLaunchKernelGGL(nwc::k_keygen_sign, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const uint8_t*)d_seeds,
                      (const uint8_t*)d_msgs, n, (uint8_t*)d_pks, (uint8_t*)d_sigs, d.base_table);
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+
+int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t n, const uint32_t* worker_offsets,
+                             const uint32_t* worker_ids) {
+  if (int rc = require_init()) return rc;
+  if (n && (!pks || !stakes || !worker_offsets)) return set_err(NWC_ERR_ARG, "null buffer");
+  if (n && worker_offsets[0] != 0) return set_err(NWC_ERR_ARG, "worker_offsets[0] must be 0");
+  for (size_t k = 0; k < n; ++k)
+    if (worker_offsets[k + 1] < worker_offsets[k]) return set_err(NWC_ERR_ARG, "worker_offsets not monotone");
+  const uint32_t nw = n ? worker_offsets[n] : 0;
+  if (nw && !worker_ids) return set_err(NWC_ERR_ARG, "null worker ids");
+  // the key cache indexes authorities by their position in `pks` (a duplicate key keeps its
+  // first position, as the committee's BTreeMap would hold one entry)
+  if (int rc = nwc_set_committee(pks, n)) return rc;
+  uint64_t total = 0;
+  for (size_t k = 0; k < n; ++k) total += stakes[k];
+  for (auto& dp : g_devs) {
+    DevCtx& d = *dp;
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    if (d.cc_stakes) HIP_TRY(hipFree(d.cc_stakes));
+    if (d.cc_worker_off) HIP_TRY(hipFree(d.cc_worker_off));
+    if (d.cc_worker_ids) HIP_TRY(hipFree(d.cc_worker_ids));
+    d.cc_stakes = nullptr; d.cc_worker_off = nullptr; d.cc_worker_ids = nullptr;
+    d.cc_n = 0;
+    d.cc_quorum = 2 * total / 3 + 1;   // Committee::quorum_threshold (config/src/lib.rs:168-173)
+    HIP_TRY(hipMalloc(&d.cc_stakes, 8 * (n + 1)));
+    HIP_TRY(hipMalloc(&d.cc_worker_off, 4 * (n + 1)));
+    HIP_TRY(hipMalloc(&d.cc_worker_ids, 4 * (size_t)(nw + 1)));
+    if (n) {
+      HIP_TRY(hipMemcpy(d.cc_stakes, stakes, 8 * n, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(d.cc_worker_off, worker_offsets, 4 * (n + 1), hipMemcpyHostToDevice));
+      if (nw) HIP_TRY(hipMemcpy(d.cc_worker_ids, worker_ids, 4 * (size_t)nw, hipMemcpyHostToDevice));
+    }
+    d.cc_n = (uint32_t)n;
+  }
+  return 0;
+}
+
+int nwc_sanitize_messages(const uint8_t* data, const uint64_t* offsets, size_t m, uint64_t gc_round,
+                          const uint8_t* vote_target, int32_t* codes, uint8_t* digests32, uint8_t* kinds) {
+  if (int rc = require_init()) return rc;
+  if (m == 0) return 0;
+  if (!data || !offsets || !codes) return set_err(NWC_ERR_ARG, "null buffer");
+  for (size_t i = 0; i < m; ++i)
+    if (offsets[i + 1] < offsets[i]) return set_err(NWC_ERR_ARG, "offsets not monotone at %zu", i);
+  const uint64_t base = offsets[0], total = offsets[m] - base;
+  DevCtx& d = *ctx(t_dev < (int)g_devs.size() ? t_dev : 0);
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  if (!d.cc_stakes) return set_err(NWC_ERR_NOT_INIT, "nwc_set_committee_config has not been called");
+  const uint64_t vcap = total / 116 + 1;
+  const uint32_t used_words = (d.cc_n + 31) / 32 + 1;
+  const size_t need = align256(total + 16) + align256(8 * (m + 1)) + align256(total + 128 * (m + 2)) +
+                      align256(32 * m) * 3 + align256(64 * m) + align256(32 * vcap) + align256(64 * vcap) +
+                      align256(4 * vcap) + align256(4) + align256(4 * (size_t)used_words * m) + align256(16 * m) +
+                      align256(4 * m) + align256(8 * ((m + 63) / 64)) + align256(8 * ((vcap + 63) / 64)) +
+                      align256(4 * m) + align256(32 * m);
+  if (need > d.msg_arena_cap) {
+    HIP_TRY(hipEventSynchronize(d.scratch_free));
+    if (d.msg_arena) HIP_TRY(hipFree(d.msg_arena));
+    d.msg_arena = nullptr;
+    d.msg_arena_cap = 0;
+    const size_t cap = need + need / 4 + (1 << 20);
+    HIP_TRY(hipMalloc(&d.msg_arena, cap));
+    d.msg_arena_cap = cap;
+  }
+  Carve c(d.msg_arena);
+  uint8_t* ddata = c.take<uint8_t>(total + 16);
+  uint64_t* doff = c.take<uint64_t>(8 * (m + 1));
+  nwc::MsgArgs a{};
+  a.data = ddata;
+  a.offsets = doff;
+  a.m = m;
+  a.gc_round = gc_round;
+  a.hashbuf = c.take<uint8_t>(total + 128 * (m + 2));
+  a.eq_msg = c.take<uint8_t>(32 * m);
+  a.eq_pk = c.take<uint8_t>(32 * m);
+  a.eq_sig = c.take<uint8_t>(64 * m);
+  a.cdig = c.take<uint8_t>(32 * m);
+  a.v_pk = c.take<uint8_t>(32 * vcap);
+  a.v_sig = c.take<uint8_t>(64 * vcap);
+  a.v_msg = c.take<uint32_t>(4 * vcap);
+  a.v_total = c.take<uint32_t>(4);
+  a.v_cap = vcap;
+  a.used = c.take<uint32_t>(4 * (size_t)used_words * m);
+  a.used_words = used_words;
+  a.rec = c.take<uint32_t>(16 * m);
+  a.rec_n = c.take<uint32_t>(4 * m);
+  uint64_t* sbits = c.take<uint64_t>(8 * ((m + 63) / 64));
+  uint64_t* lbits = c.take<uint64_t>(8 * ((vcap + 63) / 64));
+  int32_t* dcodes = c.take<int32_t>(4 * m);
+  a.digests = digests32 ? c.take<uint8_t>(32 * m) : nullptr;
+  if (vote_target) {
+    a.target.enabled = 1;
+    std::memcpy(a.target.id, vote_target, 32);
+    std::memcpy(&a.target.round, vote_target + 32, 8);
+    std::memcpy(a.target.origin, vote_target + 40, 32);
+  }
+  // stage: message bytes (rebased to 0) and offsets
+  std::vector<uint64_t> hoff(m + 1);
+  for (size_t i = 0; i <= m; ++i) hoff[i] = offsets[i] - base;
+  HIP_TRY(hipMemcpyAsync(ddata, data + base, total, hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(hipMemsetAsync(ddata + total, 0, 16, d.stream));
+  HIP_TRY(hipMemcpyAsync(doff, hoff.data(), 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(hipMemsetAsync(a.v_total, 0, 4, d.stream));
+  HIP_TRY(hipMemsetAsync(a.v_msg, 0, 4 * vcap, d.stream));
+  const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
+  const nwc::CommitteeCfg cc{d.cc_stakes, d.cc_worker_off, d.cc_worker_ids, d.cc_quorum, d.cc_n};
+  hipLaunchKernelGGL(nwc::k_parse_messages, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.stream, a, cm, cc);
+  HIP_TRY(hipGetLastError());
+  uint32_t nv = 0;
+  HIP_TRY(hipMemcpyAsync(&nv, a.v_total, 4, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  const uint64_t nvotes = std::min<uint64_t>(nv, vcap);
+  // the signature equations: strict (headers' and votes' signatures), batch leaves (votes)
+  if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, m, 1, sbits, d.stream)) return rc;
+  if (nvotes)
+    if (int rc = launch_verify(d, a.cdig, a.v_msg, 0, a.v_pk, a.v_sig, nvotes, 0, lbits, d.stream)) return rc;
+  hipLaunchKernelGGL(nwc::k_finalize_messages, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.stream, a.rec,
+                     a.rec_n, sbits, lbits, (uint64_t)m, dcodes);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(codes, dcodes, 4 * m, hipMemcpyDeviceToHost, d.stream));
+  std::vector<uint32_t> rec;
+  if (kinds) {
+    rec.resize(4 * m);
+    HIP_TRY(hipMemcpyAsync(rec.data(), a.rec, 16 * m, hipMemcpyDeviceToHost, d.stream));
+  }
+  if (digests32) HIP_TRY(hipMemcpyAsync(digests32, a.digests, 32 * m, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  if (kinds)
+    for (size_t i = 0; i < m; ++i) kinds[i] = (uint8_t)rec[4 * i];
   return 0;
 }
 
