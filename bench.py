@@ -246,6 +246,102 @@ def bench_cfg3(lib, m: int, steps: int):
     return out
 
 
+def make_cfg3_wire(m: int, N: int = 100, Q: int = 67):
+    """cfg 3 as the primary receives it: m bincode `PrimaryMessage::Certificate`s of a 100-node
+    committee (stake 1, worker 0), each header with 67 parents, 67 votes by distinct members, 1 %
+    of votes invalid (signed over another digest).  Fixed layout (10,100 B per certificate):
+      0 u32 variant 2 | 4 str author (u64 44 + base64) | 56 u64 round | 64 u64 P = 0 |
+      72 u64 Q = 67 | 80 parents 67 x 32 | 2224 id | 2256 signature | 2320 u64 V = 67 |
+      2328 V x (u64 44, base64 key, 64-B signature)
+    Keys and signatures come from the GPU signer; digests from hashlib (workload construction)."""
+    import base64
+    import torch
+    from narwhal_amd import device
+    cseeds = device.derive32(b"nw-committee", 0, N)
+    cpk, _ = device.keygen_sign(cseeds, torch.zeros((N, 32), dtype=torch.uint8, device="cuda"))
+    cpk_h = cpk.cpu().numpy()
+    b64 = np.frombuffer(b"".join(base64.b64encode(k.tobytes()) for k in cpk_h), np.uint8).reshape(N, 44)
+    rng = np.random.default_rng(0x4E57)
+    author = rng.integers(0, N, m)
+    voters = np.argsort(rng.random((m, N)), axis=1)[:, :Q]
+    rounds = (np.arange(m, dtype=np.uint64) % 1000) + 1
+    parents = rng.integers(0, 256, (m, Q, 32), dtype=np.uint8)
+    ids = np.empty((m, 32), np.uint8)
+    cdig = np.empty((m, 32), np.uint8)
+    for c in range(m):
+        a32 = cpk_h[author[c]].tobytes()
+        r8 = int(rounds[c]).to_bytes(8, "little")
+        ids[c] = np.frombuffer(hashlib.sha512(a32 + r8 + parents[c].tobytes()).digest()[:32], np.uint8)
+        cdig[c] = np.frombuffer(hashlib.sha512(ids[c].tobytes() + r8 + a32).digest()[:32], np.uint8)
+    t_ids, t_cd = torch.from_numpy(ids).cuda(), torch.from_numpy(cdig).cuda()
+    _, hsig = device.keygen_sign(cseeds[torch.from_numpy(author).cuda()].contiguous(), t_ids)
+    signed = t_cd.repeat_interleave(Q, dim=0)
+    bad = torch.from_numpy(rng.random(m * Q) < 0.01).cuda()
+    signed[bad, 0] ^= 1
+    _, vsig = device.keygen_sign(cseeds[torch.from_numpy(voters.reshape(-1)).cuda()].contiguous(), signed)
+    SZ = 2328 + Q * 116
+    buf = np.zeros((m, SZ), np.uint8)
+    buf[:, 0:4] = np.frombuffer((2).to_bytes(4, "little"), np.uint8)
+    buf[:, 4:12] = np.frombuffer((44).to_bytes(8, "little"), np.uint8)
+    buf[:, 12:56] = b64[author]
+    buf[:, 56:64] = rounds.view(np.uint8).reshape(m, 8)
+    buf[:, 72:80] = np.frombuffer(Q.to_bytes(8, "little"), np.uint8)
+    buf[:, 80:2224] = parents.reshape(m, Q * 32)
+    buf[:, 2224:2256] = ids
+    buf[:, 2256:2320] = hsig.cpu().numpy()
+    buf[:, 2320:2328] = np.frombuffer(Q.to_bytes(8, "little"), np.uint8)
+    votes = buf[:, 2328:].reshape(m, Q, 116)
+    votes[:, :, 0:8] = np.frombuffer((44).to_bytes(8, "little"), np.uint8)
+    votes[:, :, 8:52] = b64[voters]
+    votes[:, :, 52:116] = vsig.cpu().numpy().reshape(m, Q, 64)
+    exp_bad_cert = bad.view(m, Q).any(dim=1).cpu().numpy()
+    return buf, cpk_h, exp_bad_cert
+
+
+def bench_cfg3_wire(lib, m: int, steps: int):
+    """Core::sanitize_certificate for m wire certificates (nwc_dev_sanitize_messages, bytes resident in
+    HBM): decode + digests + committee checks + header signature + 67 vote leaves per certificate."""
+    from narwhal_amd import _lib
+    import torch
+    N = 100
+    buf, cpk, exp_bad = make_cfg3_wire(m, N)
+    n_ = len(cpk)
+    offs_c = (ctypes.c_uint32 * (n_ + 1))(*range(n_ + 1))
+    _lib.check(lib.nwc_set_committee_config(_lib.buf(np.ascontiguousarray(cpk)), (ctypes.c_uint64 * n_)(*([1] * n_)),
+                                            n_, offs_c, (ctypes.c_uint32 * n_)(*([0] * n_))))
+    SZ = buf.shape[1]
+    data = torch.zeros(m * SZ + 64, dtype=torch.uint8, device="cuda")
+    data[:m * SZ] = torch.from_numpy(buf.reshape(-1)).cuda()
+    offs = torch.arange(m + 1, dtype=torch.int64, device="cuda") * SZ
+    codes = torch.empty(m, dtype=torch.int32, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    run = lambda: _lib.check(lib.nwc_dev_sanitize_messages(  # noqa: E731
+        ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(offs.data_ptr()), m, m * SZ, 0, None,
+        ctypes.c_void_p(codes.data_ptr()), None, stream))
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    got = codes.cpu().numpy()
+    ok = bool(((got == 1) == exp_bad).all() and ((got == 0) == ~exp_bad).all())
+    # host ABI (wire bytes in host memory, PCIe-inclusive)
+    hoffs = np.arange(m + 1, dtype=np.uint64) * SZ
+    hcodes = np.zeros(m, np.int32)
+    flat = buf.reshape(-1)
+    t0 = time.perf_counter()
+    _lib.check(lib.nwc_sanitize_messages(_lib.buf(flat), _lib.buf(hoffs), m, 0, None, _lib.buf(hcodes), None, None))
+    hdt = time.perf_counter() - t0
+    _lib.check(lib.nwc_set_committee(None, 0))
+    return {"workload": "cfg3 wire: %d bincode Certificate messages (100-node committee, 67 parents, 67 votes, "
+                        "1%% bad votes) -> DagError codes" % m,
+            "certs_per_s": m / dt, "votes_per_s": m * 67 / dt, "ms_per_step": dt * 1e3,
+            "wire_GBps": m * SZ / dt / 1e9, "parity_ok": ok and bool((hcodes == got).all()),
+            "host_abi_certs_per_s": m / hdt, "failing_certs": int(exp_bad.sum())}
+
+
 # ---- timing ----------------------------------------------------------------------------------
 def timed_kernel(fn, iters: int):
     """Average duration (ms) of fn() launches measured with HIP events on torch's current
@@ -320,6 +416,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU-baseline leg (0 = skip)")
     ap.add_argument("--cfg3-certs", type=int, default=100000, help="config 3 certificates (0 = skip)")
     ap.add_argument("--cfg1-calls", type=int, default=2000, help="config 1 latency calls (0 = skip)")
+    ap.add_argument("--wire-certs", type=int, default=20000, help="cfg 3 from wire bytes (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -391,6 +488,8 @@ def main():
         extras["cfg3"] = bench_cfg3(lib, args.cfg3_certs, max(1, args.steps // 2))
     if world == 1 and args.cfg1_calls > 0:
         extras["cfg1"] = bench_cfg1(lib, args.cfg1_calls)
+    if world == 1 and args.wire_certs > 0:
+        extras["cfg3_wire"] = bench_cfg3_wire(lib, args.wire_certs, max(1, args.steps // 2))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:

@@ -77,7 +77,8 @@ int nwc_set_committee(const uint8_t* pks, size_t n);
 /* config::Committee for the message checks (config/src/lib.rs:134-212): n authorities with
  * their keys, stakes (Committee::stake) and worker ids (Committee::worker): authority k runs
  * workers worker_ids[worker_offsets[k] .. worker_offsets[k+1]).  Also sets the key cache
- * (nwc_set_committee); a later nwc_set_committee drops the stake/worker tables. */
+ * (nwc_set_committee); a later nwc_set_committee drops the stake/worker tables.  At most 4096
+ * authorities. */
 int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t n,
                              const uint32_t* worker_offsets, const uint32_t* worker_ids);
 
@@ -106,6 +107,13 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
  * 0 header, 1 vote, 2 certificate, 3 other.  Needs nwc_set_committee_config. */
 int nwc_sanitize_messages(const uint8_t* data, const uint64_t* offsets, size_t m, uint64_t gc_round,
                           const uint8_t* vote_target, int32_t* codes, uint8_t* digests32, uint8_t* kinds);
+
+/* Device-resident variant: d_data (4-byte aligned, >= 16 readable bytes past the last message)
+ * and d_offsets (device u64[m+1], d_offsets[0] = 0, d_offsets[m] = total) in HBM; d_codes device
+ * i32[m], d_digests32 (nullable) device m x 32 B.  Synchronises once (the vote count). */
+int nwc_dev_sanitize_messages(const void* d_data, const void* d_offsets, uint64_t m, uint64_t total,
+                              uint64_t gc_round, const uint8_t* vote_target, void* d_codes,
+                              void* d_digests32, void* stream);
 
 /* ---- digests -------------------------------------------------------------------------- */
 /* Sha512::digest(bytes)[..32] -- worker/src/processor.rs:38 and crypto's `Hash for &[u8]`

@@ -52,6 +52,9 @@ _SIGS = {
                                            ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_dev_set_device": (ctypes.c_int, [ctypes.c_int]),
     "nwc_set_committee_config": (ctypes.c_int, [_c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p, _c_u8p]),
+    "nwc_dev_sanitize_messages": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.c_uint64, _c_u8p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p]),
     "nwc_sanitize_messages": (ctypes.c_int, [_c_u8p, _c_u8p, ctypes.c_size_t, ctypes.c_uint64, _c_u8p, _c_u8p,
                                              _c_u8p, _c_u8p]),
 }

@@ -1,17 +1,19 @@
 // Primary messages on the GPU: bincode/base64 ingestion, message digests and the structural
 // checks of Header::verify / Vote::verify / Certificate::verify.
 //
-//   k_parse_messages     one lane per serialized PrimaryMessage (bincode 1.3 legacy config:
-//                        little-endian fixint, u64 lengths; primary/src/primary.rs:230):
-//                        decodes the message, the base64 PublicKey strings
-//                        (crypto/src/lib.rs:94-112), computes Header::digest
-//                        (primary/src/messages.rs:70-84), Vote::digest (:145-153) and
-//                        Certificate::digest (:226-234), applies the committee checks in the
-//                        reference's order, and emits the signature equations: one strict
-//                        equation per message (the header's or the vote's signature) and one
-//                        batch-leaf equation per certificate vote.
-//   k_finalize_messages  combines the structural code with the equation verdicts into the
-//                        DagError the reference returns (primary/src/error.rs).
+//   k_parse_messages     one wave per serialized PrimaryMessage (bincode 1.3 legacy config:
+//                        little-endian fixint, u64 lengths; primary/src/primary.rs:230): the
+//                        fixed fields are decoded by every lane alike, the certificate's votes
+//                        one per lane (a vote is 116 B once its key string is 44 B, so vote v
+//                        sits at a computed offset); decodes the base64 PublicKeys
+//                        (crypto/src/lib.rs:94-112), gathers the Header::digest input
+//                        (primary/src/messages.rs:70-84), computes Vote::digest (:145-153) and
+//                        Certificate::digest (:226-234), evaluates the committee checks, and emits
+//                        the signature equations: one strict equation per message (the header's
+//                        or the vote's signature) and one batch-leaf equation per certificate vote.
+//   k_header_digests     one lane per message: Header::digest of the gathered input vs the id.
+//   k_finalize_messages  combines the flags with the equation verdicts into the DagError the
+//                        reference returns, in its order (primary/src/error.rs).
 //
 // Wire layout (bincode of PrimaryMessage, primary/src/primary.rs:33-38):
 //   u32 variant (0 Header, 1 Vote, 2 Certificate, 3 CertificatesRequest)
@@ -76,10 +78,9 @@ struct MsgArgs {
   uint8_t* cdig;                // m x 32: Certificate::digest per message (votes sign it)
   uint32_t* v_total;            // atomic vote-slot allocator
   uint64_t v_cap;
-  uint32_t* used;               // m x used_words: AuthorityReuse bitmaps
-  uint32_t used_words;
-  uint32_t* rec;                // m x 4: kind, pre code, post code, vote base
+  uint32_t* rec;                // m x 4: kind | flags << 8, post code, vote base, header digest input length
   uint32_t* rec_n;              // m: vote count
+  uint32_t* hmatch;             // m: Header::digest == id (k_header_digests)
   uint8_t* digests;             // m x 32: the message's digest (Header::digest / Vote::digest /
                                 //         Certificate::digest), for the caller
 };
@@ -235,132 +236,154 @@ __device__ __forceinline__ uint64_t member_stake(const CommitteeCfg& cc, int idx
   return idx >= 0 ? cc.stakes[idx] : 0;
 }
 
-// Header fields shared by Header and Certificate messages (reader positioned at the header).
-struct HeaderView {
-  u32 author[8], id[8], sig[16], digest[8];
-  uint64_t round;
-  int aidx;            // committee index of the author (-1: not a member)
-  bool worker_bad;     // a payload worker id the author does not run (MalformedHeader)
+// committees of up to this many authorities (the AuthorityReuse scan keeps one LDS slot each)
+constexpr uint32_t MSG_MAX_COMMITTEE = 4096;
+enum MsgFlag : u32 {
+  MF_PARSE_ERR = 1u << 8,    // bincode / base64 decoding failed
+  MF_GENESIS = 1u << 9,      // Certificate::genesis(committee).contains(self)
+  MF_TOO_OLD = 1u << 10,     // gc_round > round (header, certificate)
+  MF_STAKE0 = 1u << 11,      // the author has no voting rights
+  MF_WORKER_BAD = 1u << 12,  // a payload worker id the author does not run
 };
-__device__ void parse_header(MsgReader& r, const Committee& cm, const CommitteeCfg& cc, uint8_t* hb, HeaderView& h) {
-  r.key(h.author);
-  const uint64_t round_off = r.pos;
-  h.round = r.u64();
-  const uint64_t P = r.u64();
-  r.need(P <= (1ull << 40) ? P * 36 : ~0ull);
-  const uint64_t pay_off = r.pos;
-  if (r.ok) r.pos += P * 36;
-  const uint64_t Q = r.u64();
-  r.need(Q <= (1ull << 40) ? Q * 32 : ~0ull);
-  const uint64_t par_off = r.pos;
-  if (r.ok) r.pos += Q * 32;
-  r.bytes32(h.id);
-  r.bytes64(h.sig);
-  h.aidx = r.ok ? committee_lookup(cm, h.author) : -1;
-  h.worker_bad = false;
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) h.digest[i] = 0;
-  if (!r.ok) return;
-  // worker ids (Committee::worker(author, id)); only consulted when the author is a member
-  if (h.aidx >= 0) {
-    const uint32_t w0 = cc.worker_off[h.aidx], w1 = cc.worker_off[h.aidx + 1];
-    for (uint64_t e = 0; e < P; ++e) {
-      const u32 wid = ld_u32(r.base, pay_off + 36 * e + 32);
-      bool found = false;
-      for (uint32_t k = w0; k < w1; ++k) found = found || (cc.worker_ids[k] == wid);
-      h.worker_bad = h.worker_bad || !found;
-    }
+
+__device__ __forceinline__ u32 wave_min_u32(u32 v) {
+  _Pragma("unroll") for (int m = 32; m >= 1; m >>= 1) v = min(v, (u32)__shfl_xor((int)v, m, 64));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+  _Pragma("unroll") for (int m = 32; m >= 1; m >>= 1) {
+    const u32 lo = (u32)__shfl_xor((int)(u32)v, m, 64), hi = (u32)__shfl_xor((int)(u32)(v >> 32), m, 64);
+    v += (uint64_t)lo | ((uint64_t)hi << 32);
   }
-  // Header::digest input: author(32) || round(8) || payload entries (36 each) || parents (32 each),
-  // gathered into the 128-B-aligned scratch hb (every destination offset is a multiple of 4)
-  u32* d = reinterpret_cast<u32*>(hb);
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) d[i] = h.author[i];
-  d[8] = (u32)h.round;
-  d[9] = (u32)(h.round >> 32);
-  (void)round_off;
-  const uint64_t pw = P * 9, qw = Q * 8;
-  for (uint64_t k = 0; k < pw; ++k) d[10 + k] = ld_u32(r.base, pay_off + 4 * k);
-  for (uint64_t k = 0; k < qw; ++k) d[10 + pw + k] = ld_u32(r.base, par_off + 4 * k);
-  sha512_trunc32_buf(hb, 40 + 36 * P + 32 * Q, h.digest);
+  return v;
 }
 
-__global__ __launch_bounds__(256) void k_parse_messages(MsgArgs a, Committee cm, CommitteeCfg cc) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.m) return;
+// One wave (64-thread block) per message.  Every lane runs the sequential field decoding (same
+// instructions, no divergence); vote-, payload- and digest-input loops are split across lanes.
+__global__ __launch_bounds__(64) void k_parse_messages(MsgArgs a, Committee cm, CommitteeCfg cc) {
+  __shared__ u32 first[MSG_MAX_COMMITTEE];   // first vote position of each committee member
+  const uint64_t i = blockIdx.x;
+  const u32 lane = threadIdx.x;
+  if (i >= a.m) return;   // block-uniform
   MsgReader r{a.data, a.offsets[i], a.offsets[i + 1], true};
   const uint64_t variant = ld_u32(a.data, r.pos);
   r.need(4);
   r.pos += 4;
-  u32 kind = variant <= 2 ? (u32)variant : (u32)MSG_OTHER;
-  if (!r.ok) kind = MSG_OTHER;
-  u32 pre = DAG_OK, post = DAG_OK, vbase = 0, vcount = 0;
+  u32 kind = (r.ok && variant <= 2) ? (u32)variant : (u32)MSG_OTHER;
+  u32 flags = 0, post = DAG_OK, vbase = 0, vcount = 0, hlen = 0;
   u32 eq_msg[8], eq_pk[8], eq_sig[16], dig[8], cd[8];
   _Pragma("unroll") for (int k = 0; k < 8; ++k) { eq_msg[k] = 0; eq_pk[k] = 0; dig[k] = 0; cd[k] = 0; }
   _Pragma("unroll") for (int k = 0; k < 16; ++k) eq_sig[k] = 0;
-  uint8_t* hb = a.hashbuf + ((a.offsets[i] + 127) & ~(uint64_t)127) + 128 * i;
   if (kind == MSG_HEADER || kind == MSG_CERTIFICATE) {
-    HeaderView h;
-    parse_header(r, cm, cc, hb, h);
-    // Certificate: votes
-    uint64_t V = 0;
-    bool reuse_first = false, unknown_first = false;
-    uint64_t weight = 0;
-    if (kind == MSG_CERTIFICATE) {
-      V = r.u64();
-      r.need(V <= (1ull << 32) ? V * 116 : ~0ull);   // >= 116 bytes per vote
-      if (r.ok) {
-        vbase = atomicAdd(a.v_total, (uint32_t)V);
-        if ((uint64_t)vbase + V > a.v_cap) { r.ok = false; vbase = 0; }
-      }
-      digest72(h.id, h.round, h.author, cd);
-      uint32_t* used = a.used + i * a.used_words;
-      for (u32 k = 0; k < a.used_words; ++k) used[k] = 0;
-      bool vote_err = false;
-      for (uint64_t v = 0; v < V && r.ok; ++v) {
-        u32 key[8], sg[16];
-        r.key(key);
-        r.bytes64(sg);
-        if (!r.ok) break;
-        st_words(a.v_pk + 32 * (vbase + v), key, 8);
-        st_words(a.v_sig + 64 * (vbase + v), sg, 16);
-        a.v_msg[vbase + v] = (uint32_t)i;
-        // Certificate::verify (primary/src/messages.rs:198-208): reuse, then stake, in vote order
-        if (!vote_err) {
-          const int kidx = committee_lookup(cm, key);
-          const uint64_t st = member_stake(cc, kidx);
-          const bool reused = kidx >= 0 && ((used[kidx >> 5] >> (kidx & 31)) & 1);
-          if (reused) { reuse_first = true; vote_err = true; }
-          else if (st == 0) { unknown_first = true; vote_err = true; }
-          else { used[kidx >> 5] |= 1u << (kidx & 31); weight += st; }
+    u32 author[8], id[8], sig[16];
+    r.key(author);
+    const uint64_t round = r.u64();
+    const uint64_t P = r.u64();
+    r.need(P <= (1ull << 40) ? P * 36 : ~0ull);
+    const uint64_t pay_off = r.pos;
+    if (r.ok) r.pos += P * 36;
+    const uint64_t Q = r.u64();
+    r.need(Q <= (1ull << 40) ? Q * 32 : ~0ull);
+    const uint64_t par_off = r.pos;
+    if (r.ok) r.pos += Q * 32;
+    r.bytes32(id);
+    r.bytes64(sig);
+    const int aidx = r.ok ? committee_lookup(cm, author) : -1;
+    const uint64_t astake = member_stake(cc, aidx);
+    if (r.ok) {
+      // Committee::worker(author, id) for every payload entry (only consulted for members)
+      bool wbad = false;
+      if (aidx >= 0) {
+        const uint32_t w0 = cc.worker_off[aidx], w1 = cc.worker_off[aidx + 1];
+        for (uint64_t e = lane; e < P; e += 64) {
+          const u32 wid = ld_u32(r.base, pay_off + 36 * e + 32);
+          bool found = false;
+          for (uint32_t k = w0; k < w1; ++k) found = found || (cc.worker_ids[k] == wid);
+          wbad = wbad || !found;
         }
+      }
+      if (__any(wbad)) flags |= MF_WORKER_BAD;
+      // Header::digest input gathered into the 128-B aligned scratch (word-aligned destinations)
+      uint8_t* hb = a.hashbuf + ((a.offsets[i] + 127) & ~(uint64_t)127) + 128 * i;
+      u32* d = reinterpret_cast<u32*>(hb);
+      if (lane == 0) {
+        _Pragma("unroll") for (int k = 0; k < 8; ++k) d[k] = author[k];
+        d[8] = (u32)round;
+        d[9] = (u32)(round >> 32);
+      }
+      const uint64_t pw = P * 9, qw = Q * 8;
+      for (uint64_t k = lane; k < pw; k += 64) d[10 + k] = ld_u32(r.base, pay_off + 4 * k);
+      for (uint64_t k = lane; k < qw; k += 64) d[10 + pw + k] = ld_u32(r.base, par_off + 4 * k);
+      hlen = (u32)(40 + 36 * P + 32 * Q);
+    }
+    if (kind == MSG_CERTIFICATE) {
+      const uint64_t V = r.u64();
+      r.need(V <= (1ull << 32) ? V * 116 : ~0ull);   // every vote is 116 B (44-character keys)
+      const uint64_t votes_off = r.pos;
+      if (r.ok) {
+        u32 vb = 0;
+        if (lane == 0) vb = atomicAdd(a.v_total, (uint32_t)V);
+        vbase = (u32)__shfl((int)vb, 0, 64);
+        if ((uint64_t)vbase + V > a.v_cap) r.ok = false;
+      }
+      digest72(id, round, author, cd);
+      if (r.ok) {
+        const uint32_t ncm = cc.n < MSG_MAX_COMMITTEE ? cc.n : MSG_MAX_COMMITTEE;
+        for (uint32_t k = lane; k < ncm; k += 64) first[k] = 0xFFFFFFFFu;
+        __syncthreads();
+        // pass 1: decode every vote (one per lane), emit its equation, note first positions
+        bool vok = true;
+        uint64_t weight = 0;
+        for (uint64_t v = lane; v < V; v += 64) {
+          MsgReader vr{a.data, votes_off + 116 * v, votes_off + 116 * v + 116, true};
+          u32 key[8], sg[16];
+          vr.key(key);
+          vr.bytes64(sg);
+          vok = vok && vr.ok;
+          st_words(a.v_pk + 32 * (vbase + v), key, 8);
+          st_words(a.v_sig + 64 * (vbase + v), sg, 16);
+          a.v_msg[vbase + v] = (uint32_t)i;
+          const int kidx = committee_lookup(cm, key);
+          weight += member_stake(cc, kidx);
+          if (kidx >= 0 && kidx < (int)MSG_MAX_COMMITTEE) atomicMin(&first[kidx], (u32)(v < 0xFFFFFFF0u ? v : 0xFFFFFFF0u));
+        }
+        r.ok = __all(vok);
+        __syncthreads();
+        // pass 2: Certificate::verify's vote loop (messages.rs:198-208) stops at the first vote whose
+        // name is already used (AuthorityReuse) or has no stake (UnknownAuthority); while no
+        // error has occurred every earlier vote was inserted, so "used" = all earlier names.
+        u32 err = 0xFFFFFFFFu;
+        u32 err_kind = 0;
+        for (uint64_t v = lane; v < V; v += 64) {
+          const u32* kw = reinterpret_cast<const u32*>(a.v_pk + 32 * (vbase + v));
+          u32 key[8];
+          _Pragma("unroll") for (int k = 0; k < 8; ++k) key[k] = kw[k];
+          const int kidx = committee_lookup(cm, key);
+          const bool reused = kidx >= 0 && kidx < (int)MSG_MAX_COMMITTEE && first[kidx] < (u32)v;
+          const bool unknown = member_stake(cc, kidx) == 0;
+          if ((reused || unknown) && (u32)v < err) { err = (u32)v; err_kind = reused ? DAG_AUTHORITY_REUSE : DAG_UNKNOWN_AUTHORITY; }
+        }
+        const u32 emin = wave_min_u32(err);
+        const bool mine = err == emin && emin != 0xFFFFFFFFu;
+        const uint64_t owner = __ballot(mine);
+        const u32 ek = (u32)__shfl((int)err_kind, owner ? __ffsll((unsigned long long)owner) - 1 : 0, 64);
+        const uint64_t wsum = wave_sum_u64(weight);
+        post = emin != 0xFFFFFFFFu ? ek : (wsum < cc.quorum ? DAG_REQUIRES_QUORUM : DAG_OK);
+        vcount = (u32)V;
       }
     }
     if (!r.ok) {
-      pre = DAG_SERIALIZATION;
-      V = 0;   // (slots of a truncated vote list keep the host's zero-filled v_msg: index 0 is valid)
-    } else if (kind == MSG_CERTIFICATE && h.round == 0 && h.aidx >= 0 &&
-               [&] { u32 z = 0; for (int k = 0; k < 8; ++k) z |= h.id[k]; return z == 0; }()) {
-      // genesis (Certificate::genesis(committee).contains(self), :190-193): id == 0, round 0,
-      // origin a committee member -- checked after TooOld (Core::sanitize_certificate)
-      pre = a.gc_round > h.round ? DAG_TOO_OLD : DAG_OK;
-      post = 0x100;   // marker: genesis, no signature checks
-    } else if (a.gc_round > h.round) {
-      pre = DAG_TOO_OLD;
-    } else if (!words_eq8(h.digest, h.id)) {
-      pre = DAG_INVALID_HEADER_ID;
-    } else if (member_stake(cc, h.aidx) == 0) {
-      pre = DAG_UNKNOWN_AUTHORITY;
-    } else if (h.worker_bad) {
-      pre = DAG_MALFORMED_HEADER;
+      flags |= MF_PARSE_ERR;
+      vcount = 0;   // (slots of a failed vote list keep the host's zero-filled v_msg: index 0 is valid)
+    } else {
+      u32 z = 0;
+      _Pragma("unroll") for (int k = 0; k < 8; ++k) z |= id[k];
+      if (kind == MSG_CERTIFICATE && round == 0 && aidx >= 0 && z == 0) flags |= MF_GENESIS;
+      if (a.gc_round > round) flags |= MF_TOO_OLD;
+      if (astake == 0) flags |= MF_STAKE0;
     }
-    if (kind == MSG_CERTIFICATE && post == DAG_OK) {
-      post = reuse_first ? DAG_AUTHORITY_REUSE : unknown_first ? DAG_UNKNOWN_AUTHORITY
-             : (weight < cc.quorum ? DAG_REQUIRES_QUORUM : DAG_OK);
-    }
-    vcount = (u32)V;
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) { eq_msg[k] = h.id[k]; eq_pk[k] = h.author[k]; }
-    _Pragma("unroll") for (int k = 0; k < 16; ++k) eq_sig[k] = h.sig[k];
-    if (kind == MSG_HEADER) { _Pragma("unroll") for (int k = 0; k < 8; ++k) dig[k] = h.digest[k]; }
-    else { _Pragma("unroll") for (int k = 0; k < 8; ++k) dig[k] = cd[k]; }
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) { eq_msg[k] = id[k]; eq_pk[k] = author[k]; dig[k] = cd[k]; }
+    _Pragma("unroll") for (int k = 0; k < 16; ++k) eq_sig[k] = sig[k];
   } else if (kind == MSG_VOTE) {
     u32 id[8], origin[8], author[8], sg[16];
     r.bytes32(id);
@@ -370,53 +393,97 @@ __global__ __launch_bounds__(256) void k_parse_messages(MsgArgs a, Committee cm,
     r.bytes64(sg);
     digest72(id, round, origin, dig);
     if (!r.ok) {
-      pre = DAG_SERIALIZATION;
+      flags |= MF_PARSE_ERR;
     } else if (a.target.enabled && a.target.round > round) {
-      pre = DAG_TOO_OLD;   // Core::sanitize_vote (primary/src/core.rs:319-322)
+      post = DAG_TOO_OLD;   // Core::sanitize_vote (primary/src/core.rs:319-322)
     } else if (a.target.enabled && !(words_eq8(id, a.target.id) && words_eq8(origin, a.target.origin) &&
                                      round == a.target.round)) {
-      pre = DAG_UNEXPECTED_VOTE;   // core.rs:325-330
+      post = DAG_UNEXPECTED_VOTE;   // core.rs:325-330
     } else if (member_stake(cc, committee_lookup(cm, author)) == 0) {
-      pre = DAG_UNKNOWN_AUTHORITY;   // Vote::verify (messages.rs:133-136)
+      post = DAG_UNKNOWN_AUTHORITY;   // Vote::verify (messages.rs:133-136)
     }
     _Pragma("unroll") for (int k = 0; k < 8; ++k) { eq_msg[k] = dig[k]; eq_pk[k] = author[k]; }
     _Pragma("unroll") for (int k = 0; k < 16; ++k) eq_sig[k] = sg[k];
   } else {
-    pre = r.ok && variant == 3 ? DAG_UNEXPECTED_MESSAGE : DAG_SERIALIZATION;
+    post = (r.ok && variant == 3) ? DAG_UNEXPECTED_MESSAGE : DAG_SERIALIZATION;
   }
-  st_words(a.eq_msg + 32 * i, eq_msg, 8);
-  st_words(a.eq_pk + 32 * i, eq_pk, 8);
-  st_words(a.eq_sig + 64 * i, eq_sig, 16);
-  st_words(a.cdig + 32 * i, cd, 8);
-  if (a.digests) st_words(a.digests + 32 * i, dig, 8);
-  a.rec[4 * i + 0] = kind;
-  a.rec[4 * i + 1] = pre;
-  a.rec[4 * i + 2] = post;
-  a.rec[4 * i + 3] = vbase;
-  a.rec_n[i] = vcount;
+  if (lane == 0) {
+    st_words(a.eq_msg + 32 * i, eq_msg, 8);
+    st_words(a.eq_pk + 32 * i, eq_pk, 8);
+    st_words(a.eq_sig + 64 * i, eq_sig, 16);
+    st_words(a.cdig + 32 * i, cd, 8);
+    if (a.digests && kind != MSG_HEADER) st_words(a.digests + 32 * i, dig, 8);
+    a.rec[4 * i + 0] = kind | flags;
+    a.rec[4 * i + 1] = post;
+    a.rec[4 * i + 2] = vbase;
+    a.rec[4 * i + 3] = hlen;
+    a.rec_n[i] = vcount;
+  }
 }
 
-// code[i] per the reference's order: pre (serialization, TooOld, id, authority, workers, vote
-// target) -> signature of the header / vote -> votes' reuse / stake / quorum -> verify_batch.
+// Header::digest of the gathered input, one lane per message (a header of 67 parents is 18 blocks)
+__global__ __launch_bounds__(256) void k_header_digests(MsgArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.m) return;
+  const u32 r0 = a.rec[4 * i], kind = r0 & 255u;
+  u32 match = 0;
+  if ((kind == MSG_HEADER || kind == MSG_CERTIFICATE) && !(r0 & MF_PARSE_ERR)) {
+    const uint8_t* hb = a.hashbuf + ((a.offsets[i] + 127) & ~(uint64_t)127) + 128 * i;
+    u32 dg[8], id[8];
+    sha512_trunc32_buf(hb, a.rec[4 * i + 3], dg);
+    const u32* idw = reinterpret_cast<const u32*>(a.eq_msg + 32 * i);
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) id[k] = idw[k];
+    match = words_eq8(dg, id) ? 1u : 0u;
+    if (a.digests && kind == MSG_HEADER) st_words(a.digests + 32 * i, dg, 8);
+  } else if (kind == MSG_HEADER && a.digests) {
+    u32 z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    st_words(a.digests + 32 * i, z, 8);
+  }
+  a.hmatch[i] = match;
+}
+
+// code[i] in the reference's order:
+//   header:      Serialization -> TooOld -> InvalidHeaderId -> UnknownAuthority -> MalformedHeader
+//                -> InvalidSignature                        (core.rs:306-317, messages.rs:48-67)
+//   certificate: Serialization -> TooOld -> genesis Ok -> (header checks) -> AuthorityReuse /
+//                UnknownAuthority (first vote) -> CertificateRequiresQuorum -> InvalidSignature
+//                                                            (core.rs:338-346, messages.rs:189-215)
+//   vote:        Serialization -> TooOld -> UnexpectedVote -> UnknownAuthority -> InvalidSignature
 __global__ void k_finalize_messages(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ rec_n,
-                                    const uint64_t* __restrict__ strict_bits, const uint64_t* __restrict__ leaf_bits,
-                                    uint64_t m, int32_t* __restrict__ codes) {
+                                    const uint32_t* __restrict__ hmatch, const uint64_t* __restrict__ strict_bits,
+                                    const uint64_t* __restrict__ leaf_bits, uint64_t m, int32_t* __restrict__ codes) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
-  const u32 kind = rec[4 * i], pre = rec[4 * i + 1], post = rec[4 * i + 2], vbase = rec[4 * i + 3];
+  const u32 r0 = rec[4 * i], kind = r0 & 255u, post = rec[4 * i + 1], vbase = rec[4 * i + 2];
   const u32 vn = rec_n[i];
-  u32 code = pre;
-  if (code == DAG_OK && post != 0x100) {
-    const bool sig_ok = (strict_bits[i >> 6] >> (i & 63)) & 1;
-    if (!sig_ok) code = DAG_INVALID_SIGNATURE;
-    else if (kind == MSG_CERTIFICATE) {
-      if (post != DAG_OK) code = post;
-      else {
-        bool all = true;
-        for (u32 v = vbase; v < vbase + vn; ++v) all = all && ((leaf_bits[v >> 6] >> (v & 63)) & 1);
-        code = all ? DAG_OK : DAG_INVALID_SIGNATURE;
-      }
-    }
+  const bool sig_ok = (strict_bits[i >> 6] >> (i & 63)) & 1;
+  u32 code;
+  if (kind == MSG_OTHER) {
+    code = post;
+  } else if (r0 & MF_PARSE_ERR) {
+    code = DAG_SERIALIZATION;
+  } else if (kind == MSG_VOTE) {
+    code = post != DAG_OK ? post : (sig_ok ? DAG_OK : DAG_INVALID_SIGNATURE);
+  } else if (r0 & MF_TOO_OLD) {
+    code = DAG_TOO_OLD;
+  } else if (kind == MSG_CERTIFICATE && (r0 & MF_GENESIS)) {
+    code = DAG_OK;
+  } else if (!hmatch[i]) {
+    code = DAG_INVALID_HEADER_ID;
+  } else if (r0 & MF_STAKE0) {
+    code = DAG_UNKNOWN_AUTHORITY;
+  } else if (r0 & MF_WORKER_BAD) {
+    code = DAG_MALFORMED_HEADER;
+  } else if (!sig_ok) {
+    code = DAG_INVALID_SIGNATURE;
+  } else if (kind == MSG_HEADER) {
+    code = DAG_OK;
+  } else if (post != DAG_OK) {
+    code = post;
+  } else {
+    bool all = true;
+    for (u32 v = vbase; v < vbase + vn; ++v) all = all && ((leaf_bits[v >> 6] >> (v & 63)) & 1);
+    code = all ? DAG_OK : DAG_INVALID_SIGNATURE;
   }
   codes[i] = (int32_t)code;
 }

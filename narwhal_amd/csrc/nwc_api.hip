@@ -222,12 +222,13 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * 4;
   const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
   size_t need = (size_t)cap * 256 * 2 * nwc::TAB_BYTES_PER_LANE;
-  // comb grid: resident blocks only, sized so every lane runs the same number of COMB_BATCH chunks
+  // comb grid: at most the resident blocks; tile t goes to block t mod grid, so every lane gets
+  // ceil or floor of n / lanes equations (in chunks of COMB_BATCH sharing one inversion), and
+  // a small n spreads one equation per lane
   unsigned gridc = 0;
   if (comb) {
     const uint64_t resident = (uint64_t)d.cus * d.comb_blocks_per_cu;
-    const uint64_t chunks = (tiles + resident * nwc::COMB_BATCH - 1) / (resident * nwc::COMB_BATCH);
-    gridc = (unsigned)((tiles + chunks * nwc::COMB_BATCH - 1) / (chunks * nwc::COMB_BATCH));
+    gridc = (unsigned)std::min<uint64_t>(tiles, resident);
     need = std::max(need, (size_t)resident * 256 * nwc::COMB_BYTES_PER_LANE);
   }
   if (int rc = ensure_scratch(d, need, n)) return rc;
@@ -734,6 +735,8 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
   if (int rc = require_init()) return rc;
   if (n && (!pks || !stakes || !worker_offsets)) return set_err(NWC_ERR_ARG, "null buffer");
   if (n && worker_offsets[0] != 0) return set_err(NWC_ERR_ARG, "worker_offsets[0] must be 0");
+  if (n > nwc::MSG_MAX_COMMITTEE)
+    return set_err(NWC_ERR_ARG, "committee of %zu authorities exceeds %u", n, nwc::MSG_MAX_COMMITTEE);
   for (size_t k = 0; k < n; ++k)
     if (worker_offsets[k + 1] < worker_offsets[k]) return set_err(NWC_ERR_ARG, "worker_offsets not monotone");
   const uint32_t nw = n ? worker_offsets[n] : 0;
@@ -767,27 +770,19 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
   return 0;
 }
 
-int nwc_sanitize_messages(const uint8_t* data, const uint64_t* offsets, size_t m, uint64_t gc_round,
-                          const uint8_t* vote_target, int32_t* codes, uint8_t* digests32, uint8_t* kinds) {
-  if (int rc = require_init()) return rc;
-  if (m == 0) return 0;
-  if (!data || !offsets || !codes) return set_err(NWC_ERR_ARG, "null buffer");
-  for (size_t i = 0; i < m; ++i)
-    if (offsets[i + 1] < offsets[i]) return set_err(NWC_ERR_ARG, "offsets not monotone at %zu", i);
-  const uint64_t base = offsets[0], total = offsets[m] - base;
-  DevCtx& d = *ctx(t_dev < (int)g_devs.size() ? t_dev : 0);
-  std::lock_guard<std::mutex> lk(d.mu);
-  HIP_TRY(hipSetDevice(d.hip_id));
-  if (!d.cc_stakes) return set_err(NWC_ERR_NOT_INIT, "nwc_set_committee_config has not been called");
+// Device part of nwc_sanitize_messages: messages already in HBM (ddata 4-byte aligned with >= 16
+// bytes of readable padding, doff device u64[m+1] rebased so that doff[0] is the first byte).
+// Sizes the arena from `total`; one D2H sync reads the number of vote equations.
+int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total, uint64_t gc_round,
+                 const uint8_t* vote_target, int32_t* dcodes, uint8_t* ddigests, uint32_t* drec, hipStream_t s) {
   const uint64_t vcap = total / 116 + 1;
-  const uint32_t used_words = (d.cc_n + 31) / 32 + 1;
-  const size_t need = align256(total + 16) + align256(8 * (m + 1)) + align256(total + 128 * (m + 2)) +
-                      align256(32 * m) * 3 + align256(64 * m) + align256(32 * vcap) + align256(64 * vcap) +
-                      align256(4 * vcap) + align256(4) + align256(4 * (size_t)used_words * m) + align256(16 * m) +
-                      align256(4 * m) + align256(8 * ((m + 63) / 64)) + align256(8 * ((vcap + 63) / 64)) +
-                      align256(4 * m) + align256(32 * m);
+  const size_t need = align256(total + 128 * (m + 2)) + align256(32 * m) * 3 + align256(64 * m) +
+                      align256(32 * vcap) + align256(64 * vcap) + align256(4 * vcap) + align256(4) +
+                      align256(4 * m) + align256(16 * m) + align256(4 * m) +
+                      align256(8 * ((m + 63) / 64)) + align256(8 * ((vcap + 63) / 64));
   if (need > d.msg_arena_cap) {
     HIP_TRY(hipEventSynchronize(d.scratch_free));
+    HIP_TRY(hipStreamSynchronize(s));
     if (d.msg_arena) HIP_TRY(hipFree(d.msg_arena));
     d.msg_arena = nullptr;
     d.msg_arena_cap = 0;
@@ -796,8 +791,6 @@ int nwc_sanitize_messages(const uint8_t* data, const uint64_t* offsets, size_t m
     d.msg_arena_cap = cap;
   }
   Carve c(d.msg_arena);
-  uint8_t* ddata = c.take<uint8_t>(total + 16);
-  uint64_t* doff = c.take<uint64_t>(8 * (m + 1));
   nwc::MsgArgs a{};
   a.data = ddata;
   a.offsets = doff;
@@ -813,54 +806,95 @@ int nwc_sanitize_messages(const uint8_t* data, const uint64_t* offsets, size_t m
   a.v_msg = c.take<uint32_t>(4 * vcap);
   a.v_total = c.take<uint32_t>(4);
   a.v_cap = vcap;
-  a.used = c.take<uint32_t>(4 * (size_t)used_words * m);
-  a.used_words = used_words;
-  a.rec = c.take<uint32_t>(16 * m);
+  a.hmatch = c.take<uint32_t>(4 * m);
+  a.rec = drec ? drec : c.take<uint32_t>(16 * m);
   a.rec_n = c.take<uint32_t>(4 * m);
   uint64_t* sbits = c.take<uint64_t>(8 * ((m + 63) / 64));
   uint64_t* lbits = c.take<uint64_t>(8 * ((vcap + 63) / 64));
-  int32_t* dcodes = c.take<int32_t>(4 * m);
-  a.digests = digests32 ? c.take<uint8_t>(32 * m) : nullptr;
+  a.digests = ddigests;
   if (vote_target) {
     a.target.enabled = 1;
     std::memcpy(a.target.id, vote_target, 32);
     std::memcpy(&a.target.round, vote_target + 32, 8);
     std::memcpy(a.target.origin, vote_target + 40, 32);
   }
-  // stage: message bytes (rebased to 0) and offsets
+  HIP_TRY(hipMemsetAsync(a.v_total, 0, 4, s));
+  HIP_TRY(hipMemsetAsync(a.v_msg, 0, 4 * vcap, s));
+  const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
+  const nwc::CommitteeCfg cc{d.cc_stakes, d.cc_worker_off, d.cc_worker_ids, d.cc_quorum, d.cc_n};
+  hipLaunchKernelGGL(nwc::k_parse_messages, dim3((unsigned)m), dim3(64), 0, s, a, cm, cc);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_header_digests, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  uint32_t nv = 0;
+  HIP_TRY(hipMemcpyAsync(&nv, a.v_total, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const uint64_t nvotes = std::min<uint64_t>(nv, vcap);
+  // the signature equations: strict (headers' and votes' signatures), batch leaves (votes)
+  if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, m, 1, sbits, s)) return rc;
+  if (nvotes)
+    if (int rc = launch_verify(d, a.cdig, a.v_msg, 0, a.v_pk, a.v_sig, nvotes, 0, lbits, s)) return rc;
+  hipLaunchKernelGGL(nwc::k_finalize_messages, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a.rec,
+                     a.rec_n, a.hmatch, sbits, lbits, (uint64_t)m, dcodes);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int nwc_sanitize_messages(const uint8_t* data, const uint64_t* offsets, size_t m, uint64_t gc_round,
+                          const uint8_t* vote_target, int32_t* codes, uint8_t* digests32, uint8_t* kinds) {
+  if (int rc = require_init()) return rc;
+  if (m == 0) return 0;
+  if (!data || !offsets || !codes) return set_err(NWC_ERR_ARG, "null buffer");
+  for (size_t i = 0; i < m; ++i)
+    if (offsets[i + 1] < offsets[i]) return set_err(NWC_ERR_ARG, "offsets not monotone at %zu", i);
+  const uint64_t base = offsets[0], total = offsets[m] - base;
+  DevCtx& d = *ctx(t_dev < (int)g_devs.size() ? t_dev : 0);
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  if (!d.cc_stakes) return set_err(NWC_ERR_NOT_INIT, "nwc_set_committee_config has not been called");
+  // staging area (the arena): message bytes, offsets, codes, records, digests
+  const size_t need = align256(total + 16) + align256(8 * (m + 1)) + align256(4 * m) + align256(16 * m) +
+                      align256(32 * m);
+  if (int rc = d.ensure_arena(need)) return rc;
+  Carve c(d.arena);
+  uint8_t* ddata = c.take<uint8_t>(total + 16);
+  uint64_t* doff = c.take<uint64_t>(8 * (m + 1));
+  int32_t* dcodes = c.take<int32_t>(4 * m);
+  uint32_t* drec = c.take<uint32_t>(16 * m);
+  uint8_t* ddig = digests32 ? c.take<uint8_t>(32 * m) : nullptr;
   std::vector<uint64_t> hoff(m + 1);
   for (size_t i = 0; i <= m; ++i) hoff[i] = offsets[i] - base;
   HIP_TRY(hipMemcpyAsync(ddata, data + base, total, hipMemcpyHostToDevice, d.stream));
   HIP_TRY(hipMemsetAsync(ddata + total, 0, 16, d.stream));
   HIP_TRY(hipMemcpyAsync(doff, hoff.data(), 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
-  HIP_TRY(hipMemsetAsync(a.v_total, 0, 4, d.stream));
-  HIP_TRY(hipMemsetAsync(a.v_msg, 0, 4 * vcap, d.stream));
-  const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
-  const nwc::CommitteeCfg cc{d.cc_stakes, d.cc_worker_off, d.cc_worker_ids, d.cc_quorum, d.cc_n};
-  hipLaunchKernelGGL(nwc::k_parse_messages, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.stream, a, cm, cc);
-  HIP_TRY(hipGetLastError());
-  uint32_t nv = 0;
-  HIP_TRY(hipMemcpyAsync(&nv, a.v_total, 4, hipMemcpyDeviceToHost, d.stream));
-  HIP_TRY(hipStreamSynchronize(d.stream));
-  const uint64_t nvotes = std::min<uint64_t>(nv, vcap);
-  // the signature equations: strict (headers' and votes' signatures), batch leaves (votes)
-  if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, m, 1, sbits, d.stream)) return rc;
-  if (nvotes)
-    if (int rc = launch_verify(d, a.cdig, a.v_msg, 0, a.v_pk, a.v_sig, nvotes, 0, lbits, d.stream)) return rc;
-  hipLaunchKernelGGL(nwc::k_finalize_messages, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.stream, a.rec,
-                     a.rec_n, sbits, lbits, (uint64_t)m, dcodes);
-  HIP_TRY(hipGetLastError());
+  if (int rc = sanitize_dev(d, ddata, doff, m, total, gc_round, vote_target, dcodes, ddig, drec, d.stream)) return rc;
   HIP_TRY(hipMemcpyAsync(codes, dcodes, 4 * m, hipMemcpyDeviceToHost, d.stream));
   std::vector<uint32_t> rec;
   if (kinds) {
     rec.resize(4 * m);
-    HIP_TRY(hipMemcpyAsync(rec.data(), a.rec, 16 * m, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipMemcpyAsync(rec.data(), drec, 16 * m, hipMemcpyDeviceToHost, d.stream));
   }
-  if (digests32) HIP_TRY(hipMemcpyAsync(digests32, a.digests, 32 * m, hipMemcpyDeviceToHost, d.stream));
+  if (digests32) HIP_TRY(hipMemcpyAsync(digests32, ddig, 32 * m, hipMemcpyDeviceToHost, d.stream));
   HIP_TRY(hipStreamSynchronize(d.stream));
   if (kinds)
     for (size_t i = 0; i < m; ++i) kinds[i] = (uint8_t)rec[4 * i];
   return 0;
+}
+
+int nwc_dev_sanitize_messages(const void* d_data, const void* d_offsets, uint64_t m, uint64_t total,
+                              uint64_t gc_round, const uint8_t* vote_target, void* d_codes, void* d_digests32,
+                              void* stream) {
+  if (int rc = require_init()) return rc;
+  if (m == 0) return 0;
+  if (!d_data || !d_offsets || !d_codes) return set_err(NWC_ERR_ARG, "null buffer");
+  if ((reinterpret_cast<uintptr_t>(d_data) & 3) != 0) return set_err(NWC_ERR_ARG, "d_data must be 4-byte aligned");
+  DevCtx& d = *ctx(t_dev < (int)g_devs.size() ? t_dev : 0);
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  if (!d.cc_stakes) return set_err(NWC_ERR_NOT_INIT, "nwc_set_committee_config has not been called");
+  return sanitize_dev(d, static_cast<const uint8_t*>(d_data), static_cast<const uint64_t*>(d_offsets), m, total,
+                      gc_round, vote_target, static_cast<int32_t*>(d_codes), static_cast<uint8_t*>(d_digests32),
+                      nullptr, stream ? static_cast<hipStream_t>(stream) : d.stream);
 }
 
 }  // extern "C"
