@@ -342,6 +342,74 @@ def bench_cfg3_wire(lib, m: int, steps: int):
             "host_abi_certs_per_s": m / hdt, "failing_certs": int(exp_bad.sum())}
 
 
+def bench_cfg5(lib, rank: int, world: int, total: int, steps: int):
+    """BASELINE config 5: `total` (64M) signatures sharded in contiguous ranges of total/world over
+    the ranks (strong scaling), 99 % honest-valid (cfg-2 seed scheme on the global index) and 1 %
+    edge cases spread evenly over the golden edge-case classes (tests/golden/ed25519_verify.json:
+    small-order / non-canonical A and R, s >= l, ...) with their expected strict verdicts.  Per-shard
+    verdict words are all-gathered over RCCL (timed separately) and, as the alternative, copied
+    D2H; the gather is not needed for correctness."""
+    import torch
+    from narwhal_amd import device
+    per = total // world
+    first = rank * per
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "ed25519_verify.json")))["cases"]
+    edge = [c for c in gold if len(c["msg"]) == 64 and not c["strict"]] + \
+           [c for c in gold if len(c["msg"]) == 64 and c["strict"] and "ref" not in c["name"]][:8]
+    em = torch.tensor(np.stack([np.frombuffer(bytes.fromhex(c["msg"]), np.uint8) for c in edge]), device="cuda")
+    ep = torch.tensor(np.stack([np.frombuffer(bytes.fromhex(c["pk"]), np.uint8) for c in edge]), device="cuda")
+    es = torch.tensor(np.stack([np.frombuffer(bytes.fromhex(c["sig"]), np.uint8) for c in edge]), device="cuda")
+    exp_edge = torch.tensor([bool(c["strict"]) for c in edge], device="cuda")
+    msgs = device.derive32(b"nw-msg", first, per)
+    seeds = device.derive32(b"nw-seed", first, per)
+    pks, sigs = device.keygen_sign(seeds, msgs)
+    del seeds
+    gidx = torch.arange(first, first + per, device="cuda", dtype=torch.int64)
+    slot = torch.nonzero(gidx % 100 == 37).squeeze(1)
+    cls = (gidx[slot] // 100) % len(edge)
+    msgs[slot] = em[cls]
+    pks[slot] = ep[cls]
+    sigs[slot] = es[cls]
+    expected = torch.ones(per, dtype=torch.bool, device="cuda")
+    expected[slot] = exp_edge[cls]
+    words = torch.empty(device.words_for(per), dtype=torch.int64, device="cuda")
+    run = lambda: device.verify(msgs, pks, sigs, strict=True, out=words)  # noqa: E731
+    run()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    barrier(world)
+    dt = max_over_ranks((time.perf_counter() - t0) / steps, world)
+    got = torch.from_numpy(device.unpack_bits(words, per)).cuda()
+    ok = bool((got == expected).all())
+    gather_ms = None
+    allw = None
+    if world > 1:
+        import torch.distributed as dist
+        allw = torch.empty(world * words.numel(), dtype=torch.int64, device="cuda")
+        barrier(world)
+        tg = time.perf_counter()
+        dist.all_gather_into_tensor(allw, words)
+        barrier(world)
+        gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, world)
+    td = time.perf_counter()
+    host_words = words.cpu()
+    d2h_ms = max_over_ranks((time.perf_counter() - td) * 1e3, world)
+    if allw is not None:
+        ok = ok and bool((allw[rank * words.numel():(rank + 1) * words.numel()] == words).all())
+    okt = torch.tensor([1 if ok else 0], dtype=torch.int64, device="cuda")
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    del host_words
+    return {"workload": "cfg5: %d signatures (1%% edge cases over %d golden classes) sharded %d ways, verify_strict"
+                        % (total, len(edge), world),
+            "verifies_per_s": total / dt, "ms_per_pass": dt * 1e3, "per_gpu": per, "scaling": "strong",
+            "verdict_allgather_ms": gather_ms, "verdict_d2h_ms": d2h_ms, "allgather_needed": False,
+            "edge_slots_per_gpu": int(slot.numel()), "parity_ok": bool(okt.item() == 1)}
+
+
 # ---- timing ----------------------------------------------------------------------------------
 def timed_kernel(fn, iters: int):
     """Average duration (ms) of fn() launches measured with HIP events on torch's current
@@ -417,6 +485,7 @@ def main():
     ap.add_argument("--cfg3-certs", type=int, default=100000, help="config 3 certificates (0 = skip)")
     ap.add_argument("--cfg1-calls", type=int, default=2000, help="config 1 latency calls (0 = skip)")
     ap.add_argument("--wire-certs", type=int, default=20000, help="cfg 3 from wire bytes (0 = skip)")
+    ap.add_argument("--cfg5-total", type=int, default=64 << 20, help="cfg 5 signatures over all ranks (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -484,6 +553,8 @@ def main():
                   "valu_frac": dk_gbs * 1e9 / 128 * OPS_SHA / (VALU_PEAK_TOPS * 1e12)}
 
     extras = {}
+    if args.cfg5_total > 0:
+        extras["cfg5"] = bench_cfg5(lib, rank, world, args.cfg5_total, 2)
     if world == 1 and args.cfg3_certs > 0:
         extras["cfg3"] = bench_cfg3(lib, args.cfg3_certs, max(1, args.steps // 2))
     if world == 1 and args.cfg1_calls > 0:
