@@ -24,6 +24,9 @@ def kname(full):
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    c3 = os.path.join(src, "trace_cfg3", "run_kernel_stats.csv")
+    if os.path.exists(c3):
+        shutil.copy(c3, os.path.join(dst, "kernel_stats_cfg3.csv"))
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
     summary = {}
     for name, r in stats.items():
