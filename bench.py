@@ -197,7 +197,33 @@ def bench_cfg1(lib, calls: int = 2000):
     return out
 
 
-def bench_cfg3(lib, m: int, steps: int):
+def cpu_baseline_cfg3(cdig, pks, sigs, m: int, Q: int, bad, budget_s: float):
+    """dalek 1.0.1 verify_batch (random z_i + Straus MSM, oracle/nwc_oracle.c
+    orc_verify_batch_straus) over whole certificates on the host cores, rayon-style (one
+    certificate per task), on a bounded prefix of the same certificates."""
+    from tests.oracle_lib import load_oracle
+    orc = load_oracle()
+    th = cpu_threads()
+    k = min(m, 64 * th)
+    while True:
+        offs = (np.arange(k + 1) * Q).astype(np.uint32)
+        d = cdig[:k].cpu().numpy()
+        p = pks[:k * Q].cpu().numpy()
+        s_ = sigs[:k * Q].cpu().numpy()
+        t0 = time.perf_counter()
+        got = orc.batch_straus_many(d, offs, p, s_, threads=th)
+        dt = time.perf_counter() - t0
+        if dt > budget_s / 4 or k == m:
+            break
+        k = min(m, int(k * max(2.0, budget_s / max(dt, 1e-3) * 0.8)))
+    exp = ~bad[:k * Q].view(k, Q).any(dim=1).cpu().numpy()
+    return {"value": k * Q / dt, "unit": "votes/s", "certs_per_s": k / dt, "cores": th, "kind": "port",
+            "parity_ok": bool((got == exp).all()),
+            "sample": "%d of the cfg-3 certificates (dalek verify_batch algorithm: random z, Straus MSM; "
+                      "C restatement, %d threads, %.1f s)" % (k, th, dt)}
+
+
+def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
     """BASELINE config 3: 100-node committee, m certificates x 67 votes (quorum 2N/3+1,
     config/src/lib.rs:181-186), each vote invalid with p = 0.01 (signed over another digest).
     Leaf equations for every vote + per-certificate AND; bad-vote sets checked against the
@@ -240,6 +266,8 @@ def bench_cfg3(lib, m: int, steps: int):
         ok = ok and bool((cert_ok == ~bad.view(m, Q).any(dim=1)).all())
         out[tag] = {"votes_per_s": nv / dt, "certs_per_s": m / dt, "ms_per_step": dt * 1e3, "parity_ok": ok}
     _lib.check(lib.nwc_set_committee(None, 0))
+    if cpu_budget > 0:
+        out["cpu_baseline"] = cpu_baseline_cfg3(cdig, pks, sigs, m, Q, bad, cpu_budget)
     out["workload"] = "cfg3: %d certificates x %d votes, 1%% invalid, leaf equations + certificate AND + bad-vote set" % (m, Q)
     out["bad_votes"] = int(bad.sum().item())
     out["failing_certs"] = int(bad.view(m, Q).any(dim=1).sum().item())
@@ -556,7 +584,8 @@ def main():
     if args.cfg5_total > 0:
         extras["cfg5"] = bench_cfg5(lib, rank, world, args.cfg5_total, 2)
     if world == 1 and args.cfg3_certs > 0:
-        extras["cfg3"] = bench_cfg3(lib, args.cfg3_certs, max(1, args.steps // 2))
+        extras["cfg3"] = bench_cfg3(lib, args.cfg3_certs, max(1, args.steps // 2),
+                                    args.cpu_budget / 2 if rank == 0 else 0.0)
     if world == 1 and args.cfg1_calls > 0:
         extras["cfg1"] = bench_cfg1(lib, args.cfg1_calls)
     if world == 1 and args.wire_certs > 0:

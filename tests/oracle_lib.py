@@ -28,6 +28,8 @@ class Oracle:
         for f in ("orc_verify_strict_many", "orc_leaf_many"):
             getattr(lib, f).argtypes = [vp, vp, vp, sz, vp, ctypes.c_int]
         lib.orc_verify_batch_many.argtypes = [vp, vp, vp, vp, sz, vp, vp, ctypes.c_int]
+        lib.orc_verify_batch_straus.argtypes = [vp, vp, vp, sz, ctypes.c_uint64]
+        lib.orc_verify_batch_straus_many.argtypes = [vp, vp, vp, vp, sz, vp, ctypes.c_int]
         lib.orc_digest32_many_mt.argtypes = [vp, vp, sz, vp, ctypes.c_int]
         lib.orc_keygen_sign_many.argtypes = [vp, vp, sz, sz, vp, vp, ctypes.c_int]
 
@@ -80,6 +82,16 @@ class Oracle:
         self.lib.orc_verify_batch_many(self._p(digests), self._p(offsets.astype(np.uint32)), self._p(pks),
                                        self._p(sigs), m, self._p(cert), self._p(bad), threads)
         return cert.astype(bool), bad.astype(bool)
+
+    def batch_straus_many(self, digests: np.ndarray, offsets: np.ndarray, pks: np.ndarray, sigs: np.ndarray,
+                          threads: int = 8) -> np.ndarray:
+        """dalek 1.0.1 verify_batch algorithm (random z_i, Straus MSM) per certificate."""
+        m = len(offsets) - 1
+        out = np.zeros(m, dtype=np.uint8)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint32)
+        self.lib.orc_verify_batch_straus_many(self._p(digests), self._p(offs), self._p(pks), self._p(sigs), m,
+                                              self._p(out), threads)
+        return out.astype(bool)
 
     def keygen_sign_many(self, seeds: np.ndarray, msgs: np.ndarray, threads: int = 8):
         n = seeds.shape[0]

@@ -110,3 +110,24 @@ def test_cfg4_tx_format():
     b = make_golden.cfg4_batch(0)
     assert b[:4] == b"\x00\x00\x00\x00" and int.from_bytes(b[4:12], "little") == 977
     assert int.from_bytes(b[12:20], "little") == 512 and b[20] == 1
+
+
+def test_straus_batch_port_matches_leaves(oracle):
+    """The CPU baseline's dalek verify_batch port (random z, Straus MSM) gives the deterministic-
+    domain verdict: Ok iff every leaf holds (valid certificates, prime-order bad votes, empty)."""
+    import numpy as np
+    rng = np.random.default_rng(8)
+    m, Q, N = 40, 7, 12
+    seeds = rng.integers(0, 256, (N, 32), dtype=np.uint8)
+    digests = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    voter = np.stack([rng.permutation(N)[:Q] for _ in range(m)]).reshape(-1)
+    signed = np.repeat(digests, Q, axis=0)
+    bad = rng.random(m * Q) < 0.05
+    signed[bad, 1] ^= 4
+    pks, sigs = oracle.keygen_sign_many(seeds[voter], signed)
+    sigs[3 * Q, 63] |= 0x80                       # s >= 2^255: parse failure -> Err
+    offs = (np.arange(m + 1) * Q).astype(np.uint32)
+    offs[-1] = offs[-2]                           # the last certificate is empty -> Ok
+    exp, _ = oracle.batch_many(digests, offs, pks, sigs)
+    got = oracle.batch_straus_many(digests, offs, pks, sigs)
+    assert (got == exp).all() and exp[-1] and not exp[3] and (~exp).sum() >= 3
