@@ -335,7 +335,8 @@ def bench_cfg3_wire(lib, m: int, steps: int):
     buf, cpk, exp_bad = make_cfg3_wire(m, N)
     n_ = len(cpk)
     offs_c = (ctypes.c_uint32 * (n_ + 1))(*range(n_ + 1))
-    _lib.check(lib.nwc_set_committee_config(_lib.buf(np.ascontiguousarray(cpk)), (ctypes.c_uint64 * n_)(*([1] * n_)),
+    cpk = np.ascontiguousarray(cpk)
+    _lib.check(lib.nwc_set_committee_config(_lib.buf(cpk), (ctypes.c_uint64 * n_)(*([1] * n_)),
                                             n_, offs_c, (ctypes.c_uint32 * n_)(*([0] * n_))))
     SZ = buf.shape[1]
     data = torch.zeros(m * SZ + 64, dtype=torch.uint8, device="cuda")

@@ -120,6 +120,33 @@ struct DevCtx {
 std::mutex g_mu;
 std::vector<std::unique_ptr<DevCtx>> g_devs;
 
+// Host copy of the committee key cache's lookup table (same hash and probing as the device), so
+// that small host calls can tell before launching whether every key is cached.
+struct HostCommittee {
+  std::mutex mu;
+  std::vector<nwc::u32> keys;
+  std::vector<int32_t> slots;
+  uint32_t mask = 0;
+  bool all_cached(const uint8_t* pks, uint64_t n) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (slots.empty()) return false;
+    for (uint64_t i = 0; i < n; ++i) {
+      nwc::u32 w[8];
+      std::memcpy(w, pks + 32 * i, 32);
+      const nwc::u32 h = nwc::committee_hash(w[0], w[1]);
+      bool found = false;
+      for (int p = 0; p < nwc::COMMITTEE_MAX_PROBE && !found; ++p) {
+        const int32_t idx = slots[(h + p) & mask];
+        if (idx < 0) break;
+        found = std::memcmp(&keys[8 * (size_t)idx], w, 32) == 0;
+      }
+      if (!found) return false;
+    }
+    return true;
+  }
+};
+HostCommittee g_hcm;
+
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct Carve {
@@ -211,12 +238,27 @@ int ensure_scratch(DevCtx& d, size_t bytes, uint64_t n) {
   return 0;
 }
 
+// launch_verify flags: the caller checked on the host that every key is in the committee cache,
+// and/or out_words is already zero (both let the latency path run as a single kernel)
+constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2;
+
 int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
-                  hipStream_t s) {
+                  hipStream_t s, int flags = 0) {
   if (n == 0) return 0;
   const VPath path = verify_path();
   const bool comb = path == VPath::Default && d.cm_n && d.cm_comb;
+  if (comb && n <= NWC_WIDE_MAX && (flags & LV_ALL_CACHED)) {
+    // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none)
+    const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
+    const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base16,
+                            d.scratch, d.fb_list, d.fb_count, 0u, cm};
+    const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base};
+    if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
+    hipLaunchKernelGGL(nwc::k_verify_comb_wide, dim3((unsigned)n), dim3(128), 0, s, a, ca);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   const uint64_t tiles = (n + 255) / 256;
   // persistent grid: a few blocks per resident slot so the tail is short
   const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * 4;
@@ -364,8 +406,11 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     if (msg_index) std::memcpy(h + ((uint8_t*)dmi - d.arena), msg_index + lo, 4 * n);
     std::memcpy(h + (dp - d.arena), pks + 32 * lo, 32 * n);
     std::memcpy(h + (ds - d.arena), sigs + 64 * lo, 64 * n);
-    HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena), hipMemcpyHostToDevice, d.stream));
-    if (int rc = launch_verify(d, dm, dmi, msg_stride ? 1 : 0, dp, ds, n, strict, dout, d.stream)) return rc;
+    std::memset(h + ((uint8_t*)dout - d.arena), 0, 8 * words);
+    HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena) + 8 * words, hipMemcpyHostToDevice,
+                           d.stream));
+    const int fl = LV_OUT_ZEROED | (d.cm_n && g_hcm.all_cached(pks + 32 * lo, n) ? LV_ALL_CACHED : 0);
+    if (int rc = launch_verify(d, dm, dmi, msg_stride ? 1 : 0, dp, ds, n, strict, dout, d.stream, fl)) return rc;
     HIP_TRY(hipMemcpyAsync(h, dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
     std::memcpy(out_words.data(), h, 8 * words);
@@ -561,6 +606,12 @@ int nwc_set_committee(const uint8_t* pks, size_t n) {
     if (fits) break;
     slots <<= 1;
   }
+  {
+    // host view cleared while the devices change (a call in between takes the general path),
+    // set again once every device holds the new cache (end of this function)
+    std::lock_guard<std::mutex> lk(g_hcm.mu);
+    g_hcm.slots.clear();
+  }
   for (auto& dp : g_devs) {
     DevCtx& d = *dp;
     std::lock_guard<std::mutex> lk(d.mu);
@@ -602,6 +653,12 @@ int nwc_set_committee(const uint8_t* pks, size_t n) {
     HIP_TRY(hipStreamSynchronize(d.stream));
     d.cm_n = (uint32_t)n;
     d.cm_slot_mask = slots - 1;
+  }
+  if (n) {
+    std::lock_guard<std::mutex> lk(g_hcm.mu);
+    g_hcm.keys = keys;
+    g_hcm.slots = table;
+    g_hcm.mask = slots - 1;
   }
   return 0;
 }
@@ -773,7 +830,7 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
 // Device part of nwc_sanitize_messages: messages already in HBM (ddata 4-byte aligned with >= 16
 // bytes of readable padding, doff device u64[m+1] rebased so that doff[0] is the first byte).
 // Sizes the arena from `total`; one D2H sync reads the number of vote equations.
-int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total, uint64_t gc_round,
+static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total, uint64_t gc_round,
                  const uint8_t* vote_target, int32_t* dcodes, uint8_t* ddigests, uint32_t* drec, hipStream_t s) {
   const uint64_t vcap = total / 116 + 1;
   const size_t need = align256(total + 128 * (m + 2)) + align256(32 * m) * 3 + align256(64 * m) +
@@ -840,6 +897,9 @@ int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m
   return 0;
 }
 
+static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, size_t m, uint64_t gc_round,
+                          const uint8_t* vote_target, int32_t* codes, uint8_t* digests32, uint8_t* kinds);
+
 int nwc_sanitize_messages(const uint8_t* data, const uint64_t* offsets, size_t m, uint64_t gc_round,
                           const uint8_t* vote_target, int32_t* codes, uint8_t* digests32, uint8_t* kinds) {
   if (int rc = require_init()) return rc;
@@ -847,8 +907,18 @@ int nwc_sanitize_messages(const uint8_t* data, const uint64_t* offsets, size_t m
   if (!data || !offsets || !codes) return set_err(NWC_ERR_ARG, "null buffer");
   for (size_t i = 0; i < m; ++i)
     if (offsets[i + 1] < offsets[i]) return set_err(NWC_ERR_ARG, "offsets not monotone at %zu", i);
+  // messages are independent: contiguous ranges per device, one host thread each
+  return shard(m, [&](int di, uint64_t lo, uint64_t hi) -> int {
+    return sanitize_range(di, data, offsets + lo, hi - lo, gc_round, vote_target, codes + lo,
+                          digests32 ? digests32 + 32 * lo : nullptr, kinds ? kinds + lo : nullptr);
+  });
+}
+
+static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, size_t m, uint64_t gc_round,
+                          const uint8_t* vote_target, int32_t* codes, uint8_t* digests32, uint8_t* kinds) {
+  if (m == 0) return 0;
   const uint64_t base = offsets[0], total = offsets[m] - base;
-  DevCtx& d = *ctx(t_dev < (int)g_devs.size() ? t_dev : 0);
+  DevCtx& d = *ctx(di);
   std::lock_guard<std::mutex> lk(d.mu);
   HIP_TRY(hipSetDevice(d.hip_id));
   if (!d.cc_stakes) return set_err(NWC_ERR_NOT_INIT, "nwc_set_committee_config has not been called");

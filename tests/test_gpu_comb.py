@@ -173,3 +173,39 @@ def test_comb_full_size_exact_failures(lib, oracle):
         _set_committee(lib, None)
     sub = [t[ti].cpu().numpy() for t in (msgs, pks, sigs)]
     assert not oracle.strict_many(*sub).any()
+
+
+def test_comb_small_host_calls(lib, golden_verify, oracle):
+    """Small host calls with every key cached take the single-launch latency kernel (pinned
+    staging, zeroed verdict words in the same copy); mixed batches take the general path."""
+    from narwhal_amd import _lib
+    cases, m, p, s = _golden_arrays(golden_verify)
+    committee = np.unique(p, axis=0)
+    try:
+        _set_committee(lib, committee)
+        for i, c in enumerate(cases):
+            rc = _lib.check(lib.nwc_verify_strict(_lib.buf(m[i]), _lib.buf(p[i]), _lib.buf(s[i])))
+            assert (rc == 0) == c["strict"], c["name"]
+        # batches of 1..70 votes over one digest (verify_batch leaf semantics)
+        rng = np.random.default_rng(9)
+        for n in (1, 3, 64, 65, 70):
+            idx = rng.integers(0, len(cases), n)
+            msg = m[idx[0]]
+            bad = ctypes.create_string_buffer((n + 7) // 8)
+            P, S = np.ascontiguousarray(p[idx]), np.ascontiguousarray(s[idx])   # keep the buffers alive
+            rc = _lib.check(lib.nwc_verify_batch(_lib.buf(msg), _lib.buf(P), _lib.buf(S), n, bad))
+            got_bad = np.unpackbits(np.frombuffer(bad.raw, np.uint8), bitorder="little")[:n].astype(bool)
+            exp_leaf = np.array([oracle.leaf(msg, p[j], s[j]) for j in idx])   # all votes sign `msg`
+            diff = np.nonzero(got_bad != ~exp_leaf)[0]
+            assert len(diff) == 0, (n, [(int(k), cases[idx[k]]["name"], bool(got_bad[k])) for k in diff[:8]],
+                                    cases[idx[0]]["name"])
+            assert (rc == 0) == bool(exp_leaf.all())
+        # a batch with one key outside the committee -> general path, same verdicts
+        _set_committee(lib, committee[1:])
+        outside = np.nonzero((p == committee[0]).all(axis=1))[0]
+        if len(outside):
+            i = int(outside[0])
+            rc = _lib.check(lib.nwc_verify_strict(_lib.buf(m[i]), _lib.buf(p[i]), _lib.buf(s[i])))
+            assert (rc == 0) == cases[i]["strict"]
+    finally:
+        _set_committee(lib, None)
