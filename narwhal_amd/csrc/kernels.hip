@@ -229,6 +229,29 @@ __global__ void k_build_comb(const u32* __restrict__ keys, u32 n, ge_niels_pad* 
   out[t].pad[1] = 0;
 }
 
+// Radix-2^16 basepoint comb for the throughput committee kernel: comb16[w * 32769 + j] =
+// j * 2^(16 w) * B, w = 0..15, j = 0..32768 (67 MB, MALL-resident next to the key combs): s*B is
+// 16 additions instead of 32.  One lane per entry (16w doublings, a 16-bit double-and-add, one
+// inversion), built once at nwc_init.
+constexpr int COMB16_WINDOWS = 16, COMB16_ENTRIES = 32769;
+constexpr size_t COMB16_TOTAL = (size_t)COMB16_WINDOWS * COMB16_ENTRIES;
+__global__ void k_build_comb16(ge_niels_pad* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= COMB16_TOTAL) return;
+  const int w = (int)(t / COMB16_ENTRIES), j = (int)(t % COMB16_ENTRIES);
+  ge_p3 P = ge_base_point();
+  for (int k = 0; k < 16 * w; ++k) P = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
+  const ge_cached pc = ge_p3_to_cached(P);
+  ge_p3 acc = ge_p3_identity();
+  for (int bit = 15; bit >= 0; --bit) {
+    acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
+    if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, pc));
+  }
+  out[t].n = ge_p3_to_niels(acc);
+  out[t].pad[0] = 0;
+  out[t].pad[1] = 0;
+}
+
 // ------------------------------------------------------------------------------- ladder
 // Per-lane table of the variable base in global scratch, lane-contiguous: 9 entries x 160 B
 // (cached point = 40 dwords = 10 x dwordx4).  A lookup reads one lane's 160 contiguous bytes,
@@ -722,7 +745,8 @@ struct VerifyArgs {
 struct CombArgs {
   uint32_t* list;
   uint32_t* count;
-  const ge_niels_pad* comb_base;   // basepoint comb (COMB_PER_KEY entries)
+  const ge_niels_pad* comb_base;   // radix-256 basepoint comb (COMB_PER_KEY entries; latency kernel)
+  const ge_niels_pad* comb16;      // radix-2^16 basepoint comb (COMB16_TOTAL entries; k_verify_comb)
 };
 
 __device__ __forceinline__ void load_inputs(const VerifyArgs& a, uint64_t i, u32 mw[8], u32 aw[8], u32 sgw[16]) {
@@ -814,7 +838,7 @@ __global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {
 // Equations whose key is not cached go to uc_list and are verified by k_verify in list mode.
 struct CombRec { fe X, Y, Z, P; u32 yr[8]; u32 meta; u32 pad[3]; };
 static_assert(sizeof(CombRec) == 208, "comb record layout");
-constexpr int COMB_BATCH = 8;
+constexpr int COMB_BATCH = 16;
 constexpr size_t COMB_REC_U4 = sizeof(CombRec) / 16;
 constexpr size_t COMB_BYTES_PER_LANE = COMB_BATCH * sizeof(CombRec);
 
@@ -844,33 +868,51 @@ __device__ __forceinline__ ge_p1p1 ge_niels_to_p1p1(const ge_niels& q) {
   return r;
 }
 
-// s B + k (-A) over the two combs; returns (X:Y:Z)
-__device__ __forceinline__ ge_p2 comb_sum(const u32 sw[8], const u32 kw[8], const ge_niels_pad* TB,
-                                          const ge_niels_pad* TA) {
+// s B + k (-A) with the radix-2^16 basepoint comb (16 windows) and the key's radix-256 comb
+// (32 windows): 48 additions.  Every entry is loaded one addition ahead of its use.
+__device__ __forceinline__ ge_niels comb16_load(const ge_niels_pad* tab, int w, i32 d) {
+  const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)w * COMB16_ENTRIES + (d < 0 ? -d : d));
+  union { uint4 u[8]; ge_niels_pad p; } e;
+  _Pragma("unroll") for (int c = 0; c < 8; ++c) e.u[c] = q[c];
+  return e.p.n;
+}
+__device__ __forceinline__ i32 next_digit16(u32 d[8]) {
+  const i32 v = (i32)(d[7] >> 16) - 32768;
+  digits_shl(d, 16);
+  return v;
+}
+__device__ __forceinline__ i32 next_digit8(u32 d[8]) {
+  const i32 v = (i32)(d[7] >> 24) - 128;
+  digits_shl(d, 8);
+  return v;
+}
+__device__ __forceinline__ ge_p2 comb_sum16(const u32 sw[8], const u32 kw[8], const ge_niels_pad* TB16,
+                                            const ge_niels_pad* TA) {
   u32 sd[8], kd[8];
-  sc_recode_radix256(sw, sd);
+  sc_recode_radix65536(sw, sd);
   sc_recode_radix256(kw, kd);
-  i32 ds = (i32)(sd[7] >> 24) - 128;
-  i32 dk = (i32)(kd[7] >> 24) - 128;
-  digits_shl(sd, 8);
-  digits_shl(kd, 8);
-  ge_niels nb = comb_load(TB, 31, ds);
-  ge_niels na = comb_load(TA, 31, dk);
+  i32 ds = next_digit16(sd);
+  i32 da = next_digit8(kd);
+  ge_niels nb = comb16_load(TB16, 15, ds);
+  ge_niels na = comb_load(TA, 31, da);
   ge_p1p1 t = ge_niels_to_p1p1(ge_niels_cneg(nb, ds < 0));
 #pragma unroll 1
-  for (int w = 31; w >= 0; --w) {
-    if (w != 31) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(nb, ds < 0));
-    const i32 dk_cur = dk;
-    if (w > 0) {
-      ds = (i32)(sd[7] >> 24) - 128;
-      digits_shl(sd, 8);
-      nb = comb_load(TB, w - 1, ds);
+  for (int q = 15; q >= 0; --q) {
+    // B window q (the first one started the sum), then A windows 2q+1 and 2q
+    if (q != 15) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(nb, ds < 0));
+    const i32 da_hi = da;
+    da = next_digit8(kd);
+    const ge_niels na_lo = comb_load(TA, 2 * q, da);
+    t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(na, da_hi < 0));
+    if (q > 0) {
+      ds = next_digit16(sd);
+      nb = comb16_load(TB16, q - 1, ds);
     }
-    t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(na, dk_cur < 0));
-    if (w > 0) {
-      dk = (i32)(kd[7] >> 24) - 128;
-      digits_shl(kd, 8);
-      na = comb_load(TA, w - 1, dk);
+    t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(na_lo, da < 0));
+    // two entries in flight at most: the next A entry is fetched during the next B addition
+    if (q > 0) {
+      da = next_digit8(kd);
+      na = comb_load(TA, 2 * q - 1, da);
     }
   }
   return ge_p1p1_to_p2(t);
@@ -905,7 +947,7 @@ __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs c
       const bool ok = active && key >= 0 && sc_lt_l(sw) && (fl & 1) && !small;
       u32 kw[8];
       challenge(rw, aw, mw, kw);
-      const ge_p2 q = comb_sum(sw, kw, ca.comb_base, cm.comb + (size_t)kk * COMB_PER_KEY);
+      const ge_p2 q = comb_sum16(sw, kw, ca.comb16, cm.comb + (size_t)kk * COMB_PER_KEY);
       // Z != 0 for every sum of curve points (complete formulas); a key that does not decode has
       // an off-curve comb, whose Z must not zero the lane's batched inversion
       const bool zbad = fe_is_zero(q.Z);

@@ -54,7 +54,8 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   nwc::ge_niels* base_table = nullptr;
   nwc::ge_niels_pad* base16 = nullptr;   // radix-2^16 basepoint tables (8.4 MB)
-  nwc::ge_niels_pad* comb_base = nullptr;   // basepoint comb (528 KB) for k_verify_comb
+  nwc::ge_niels_pad* comb_base = nullptr;   // radix-256 basepoint comb (528 KB): latency kernel
+  nwc::ge_niels_pad* comb16 = nullptr;      // radix-2^16 basepoint comb (67 MB): k_verify_comb
   int comb_blocks_per_cu = 1;
   uint32_t* uc_list = nullptr;     // k_verify_comb: equations whose key is not cached
   uint32_t* uc_count = nullptr;
@@ -176,6 +177,10 @@ int init_device(DevCtx& d) {
   hipLaunchKernelGGL(nwc::k_build_comb, dim3((unsigned)((nwc::COMB_PER_KEY + 255) / 256)), dim3(256), 0, d.stream,
                      (const nwc::u32*)nullptr, 1u, d.comb_base);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMalloc(&d.comb16, nwc::COMB16_TOTAL * sizeof(nwc::ge_niels_pad)));
+  hipLaunchKernelGGL(nwc::k_build_comb16, dim3((unsigned)((nwc::COMB16_TOTAL + 255) / 256)), dim3(256), 0, d.stream,
+                     d.comb16);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipMalloc(&d.base_table, 2 * 129 * sizeof(nwc::ge_niels)));
   HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
   hipLaunchKernelGGL(nwc::k_build_base_table, dim3(5), dim3(64), 0, d.stream, d.base_table);
@@ -253,7 +258,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
     const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base16,
                             d.scratch, d.fb_list, d.fb_count, 0u, cm};
-    const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base};
+    const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
     if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
     hipLaunchKernelGGL(nwc::k_verify_comb_wide, dim3((unsigned)n), dim3(128), 0, s, a, ca);
     HIP_TRY(hipGetLastError());
@@ -282,7 +287,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
   nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base16, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
-  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base};
+  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
   const bool half = path != VPath::Full;
   if (half) HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
   if (comb) {
@@ -473,6 +478,7 @@ void nwc_shutdown(void) {
     if (d->cm_slots) (void)hipFree(d->cm_slots);
     if (d->cm_comb) (void)hipFree(d->cm_comb);
     if (d->comb_base) (void)hipFree(d->comb_base);
+    if (d->comb16) (void)hipFree(d->comb16);
     if (d->pinned) (void)hipHostFree(d->pinned);
     if (d->cc_stakes) (void)hipFree(d->cc_stakes);
     if (d->cc_worker_off) (void)hipFree(d->cc_worker_off);

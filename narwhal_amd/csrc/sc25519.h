@@ -101,6 +101,22 @@ FE_DEV void sc_recode_radix256(const u32 s[8], u32 out[8]) {
   }
 }
 
+// Signed radix-2^16 digits of s < 2^253: 16 digits in [-2^15, 2^15), packed as 16-bit fields
+// (d + 2^15), digit 15 in the top half of word 7.
+FE_DEV void sc_recode_radix65536(const u32 s[8], u32 out[8]) {
+  i32 carry = 0;
+  _Pragma("unroll") for (int w = 0; w < 8; ++w) {
+    u32 packed = 0;
+    _Pragma("unroll") for (int n = 0; n < 2; ++n) {
+      i32 d = (i32)((s[w] >> (16 * n)) & 0xFFFFu) + carry;
+      carry = (d + 32768) >> 16;
+      d -= carry << 16;
+      packed |= (u32)(d + 32768) << (16 * n);
+    }
+    out[w] = packed;
+  }
+}
+
 // Shift a packed 256-bit digit string left by `bits` (top digits fall out of word 7).
 FE_DEV void digits_shl(u32 d[8], int bits) {
   _Pragma("unroll") for (int i = 7; i > 0; --i) d[i] = (d[i] << bits) | (d[i - 1] >> (32 - bits));
