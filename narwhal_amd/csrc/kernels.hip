@@ -193,18 +193,26 @@ __global__ void k_build_key_tables(const u32* __restrict__ keys, u32 n, ge_niels
 
 // ------------------------------------------------------------------------------- committee combs
 // Fixed-base combs for the doubling-free committee path (k_verify_comb): for a point P,
-//   comb[w * 129 + j] = j * 256^w * P,   w = 0..31, j = 0..128   (affine Niels, 128-B entries)
-// so that x * P = sum_w comb[w][d_w] (signed: a negative digit negates the entry) for the signed
-// radix-256 digits d_w of any x < 2^253.  P = B for the basepoint comb (528 KB, built at
-// nwc_init) and P = -A_key for each committee key (528 KB per key, built by nwc_set_committee).
-// One lane per entry: 8w doublings of P, an 8-bit double-and-add, one inversion.
-constexpr int COMB_WINDOWS = 32, COMB_ENTRIES = 129;
-constexpr size_t COMB_PER_KEY = (size_t)COMB_WINDOWS * COMB_ENTRIES;
+//   comb[w * E + j] = j * 2^(BITS w) * P,   w = 0..W-1, j = 0..E-1 = 2^(BITS-1)
+// (affine Niels, 128-B entries) so that x * P = sum_w comb[w][d_w] (a negative digit negates the
+// entry) for the signed radix-2^BITS digits d_w of any x < 2^253.
+//   BaseComb: P = B, radix 2^8, 32 windows (528 KB, nwc_init) -- the latency kernel's basepoint
+//   KeyComb:  P = -A_key, radix 2^12, 22 windows (5.8 MB per key, nwc_set_committee)
+// One lane per entry: BITS*w doublings of P, a BITS-bit double-and-add, one inversion.
+template <int BITS, int WINDOWS>
+struct CombShape {
+  static constexpr int bits = BITS, windows = WINDOWS, entries = (1 << (BITS - 1)) + 1;
+  static constexpr size_t per = (size_t)WINDOWS * entries;
+};
+using BaseComb = CombShape<8, 32>;
+using KeyComb = CombShape<12, 22>;
+constexpr size_t COMB_PER_KEY = KeyComb::per;
+template <class S>
 __global__ void k_build_comb(const u32* __restrict__ keys, u32 n, ge_niels_pad* __restrict__ out) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (size_t)(keys ? n : 1u) * COMB_PER_KEY) return;
-  const u32 key = (u32)(t / COMB_PER_KEY), r = (u32)(t % COMB_PER_KEY);
-  const int w = (int)(r / COMB_ENTRIES), j = (int)(r % COMB_ENTRIES);
+  if (t >= (size_t)(keys ? n : 1u) * S::per) return;
+  const u32 key = (u32)(t / S::per), r = (u32)(t % S::per);
+  const int w = (int)(r / S::entries), j = (int)(r % S::entries);
   ge_p3 P;
   if (keys) {
     u32 kw[8];
@@ -217,10 +225,10 @@ __global__ void k_build_comb(const u32* __restrict__ keys, u32 n, ge_niels_pad* 
   } else {
     P = ge_base_point();
   }
-  for (int k = 0; k < 8 * w; ++k) P = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
+  for (int k = 0; k < S::bits * w; ++k) P = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
   const ge_cached pc = ge_p3_to_cached(P);
   ge_p3 acc = ge_p3_identity();
-  for (int bit = 7; bit >= 0; --bit) {
+  for (int bit = S::bits - 1; bit >= 0; --bit) {
     acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
     if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, pc));
   }
@@ -842,8 +850,9 @@ constexpr int COMB_BATCH = 16;
 constexpr size_t COMB_REC_U4 = sizeof(CombRec) / 16;
 constexpr size_t COMB_BYTES_PER_LANE = COMB_BATCH * sizeof(CombRec);
 
-__device__ __forceinline__ ge_niels comb_load(const ge_niels_pad* tab, int w, i32 d) {
-  const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)w * COMB_ENTRIES + (d < 0 ? -d : d));
+// entry |d| of window w of a comb with `entries` entries per window
+__device__ __forceinline__ ge_niels comb_load(const ge_niels_pad* tab, int entries, int w, i32 d) {
+  const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)w * entries + (d < 0 ? -d : d));
   union { uint4 u[8]; ge_niels_pad p; } e;
   _Pragma("unroll") for (int c = 0; c < 8; ++c) e.u[c] = q[c];
   return e.p.n;
@@ -868,52 +877,38 @@ __device__ __forceinline__ ge_p1p1 ge_niels_to_p1p1(const ge_niels& q) {
   return r;
 }
 
-// s B + k (-A) with the radix-2^16 basepoint comb (16 windows) and the key's radix-256 comb
-// (32 windows): 48 additions.  Every entry is loaded one addition ahead of its use.
-__device__ __forceinline__ ge_niels comb16_load(const ge_niels_pad* tab, int w, i32 d) {
-  const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)w * COMB16_ENTRIES + (d < 0 ? -d : d));
-  union { uint4 u[8]; ge_niels_pad p; } e;
-  _Pragma("unroll") for (int c = 0; c < 8; ++c) e.u[c] = q[c];
-  return e.p.n;
-}
+// s B + k (-A) with the radix-2^16 basepoint comb (16 windows) and the key's radix-2^12 comb
+// (22 windows): 38 additions -- the key's windows 21..0, then B's 15..0.  Entry i+1 is fetched
+// before entry i is added, so one fetch is in flight behind every addition.
 __device__ __forceinline__ i32 next_digit16(u32 d[8]) {
   const i32 v = (i32)(d[7] >> 16) - 32768;
   digits_shl(d, 16);
   return v;
 }
-__device__ __forceinline__ i32 next_digit8(u32 d[8]) {
-  const i32 v = (i32)(d[7] >> 24) - 128;
-  digits_shl(d, 8);
-  return v;
-}
-__device__ __forceinline__ ge_p2 comb_sum16(const u32 sw[8], const u32 kw[8], const ge_niels_pad* TB16,
-                                            const ge_niels_pad* TA) {
-  u32 sd[8], kd[8];
+constexpr int COMB_SUM_ADDS = KeyComb::windows + COMB16_WINDOWS;   // 38
+__device__ __forceinline__ ge_p2 comb_sum(const u32 sw[8], const u32 kw[8], const ge_niels_pad* TB16,
+                                          const ge_niels_pad* TA) {
+  u32 sd[8], kd[9];
   sc_recode_radix65536(sw, sd);
-  sc_recode_radix256(kw, kd);
-  i32 ds = next_digit16(sd);
-  i32 da = next_digit8(kd);
-  ge_niels nb = comb16_load(TB16, 15, ds);
-  ge_niels na = comb_load(TA, 31, da);
-  ge_p1p1 t = ge_niels_to_p1p1(ge_niels_cneg(nb, ds < 0));
+  sc_recode_radix4096(kw, kd);
+  i32 d = digit4096_at(kd, KeyComb::windows - 1);
+  ge_niels e = comb_load(TA, KeyComb::entries, KeyComb::windows - 1, d);
+  ge_p1p1 t = ge_niels_to_p1p1(ge_niels_cneg(e, d < 0));
+  i32 dn = digit4096_at(kd, KeyComb::windows - 2);
+  ge_niels en = comb_load(TA, KeyComb::entries, KeyComb::windows - 2, dn);
 #pragma unroll 1
-  for (int q = 15; q >= 0; --q) {
-    // B window q (the first one started the sum), then A windows 2q+1 and 2q
-    if (q != 15) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(nb, ds < 0));
-    const i32 da_hi = da;
-    da = next_digit8(kd);
-    const ge_niels na_lo = comb_load(TA, 2 * q, da);
-    t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(na, da_hi < 0));
-    if (q > 0) {
-      ds = next_digit16(sd);
-      nb = comb16_load(TB16, q - 1, ds);
+  for (int i = 1; i < COMB_SUM_ADDS; ++i) {
+    e = en;
+    d = dn;
+    const int nx = i + 1;   // entry to fetch: key window 21 - nx, or B window 37 - nx
+    if (nx < KeyComb::windows) {
+      dn = digit4096_at(kd, KeyComb::windows - 1 - nx);
+      en = comb_load(TA, KeyComb::entries, KeyComb::windows - 1 - nx, dn);
+    } else if (nx < COMB_SUM_ADDS) {
+      dn = next_digit16(sd);
+      en = comb_load(TB16, COMB16_ENTRIES, COMB_SUM_ADDS - 1 - nx, dn);
     }
-    t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(na_lo, da < 0));
-    // two entries in flight at most: the next A entry is fetched during the next B addition
-    if (q > 0) {
-      da = next_digit8(kd);
-      na = comb_load(TA, 2 * q - 1, da);
-    }
+    t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(e, d < 0));
   }
   return ge_p1p1_to_p2(t);
 }
@@ -947,7 +942,7 @@ __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs c
       const bool ok = active && key >= 0 && sc_lt_l(sw) && (fl & 1) && !small;
       u32 kw[8];
       challenge(rw, aw, mw, kw);
-      const ge_p2 q = comb_sum16(sw, kw, ca.comb16, cm.comb + (size_t)kk * COMB_PER_KEY);
+      const ge_p2 q = comb_sum(sw, kw, ca.comb16, cm.comb + (size_t)kk * COMB_PER_KEY);
       // Z != 0 for every sum of curve points (complete formulas); a key that does not decode has
       // an off-curve comb, whose Z must not zero the lane's batched inversion
       const bool zbad = fe_is_zero(q.Z);
@@ -1026,14 +1021,18 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
       sh_rok = ok[0] && !(a.strict && ycanon_is_small_order(yc[0]));
     }
   } else {
-    u32 kw[8], sd[8], kd[8];
+    // lanes 0..31: basepoint comb (radix 2^8) windows; lanes 32..53: key comb (radix 2^12)
+    // windows; lanes 54..63 hold the identity
+    u32 kw[8], sd[8], kd[9];
     challenge(rw, aw, mw, kw);
     sc_recode_radix256(sw, sd);
-    sc_recode_radix256(kw, kd);
-    const int w = lane & 31;
+    sc_recode_radix4096(kw, kd);
     const bool bside = lane < 32;
-    const i32 d = digit256_at(bside ? sd : kd, w);
-    const ge_niels e = comb_load(bside ? ca.comb_base : cm.comb + (size_t)kk * COMB_PER_KEY, w, d);
+    const int w = bside ? lane : min(lane - 32, KeyComb::windows - 1);
+    const i32 d = bside ? digit256_at(sd, w) : digit4096_at(kd, w);
+    ge_niels e = bside ? comb_load(ca.comb_base, BaseComb::entries, w, d)
+                       : comb_load(cm.comb + (size_t)kk * COMB_PER_KEY, KeyComb::entries, w, d);
+    if (lane >= 32 + KeyComb::windows) e = ge_niels_identity();
     sum = ge_p1p1_to_p3(ge_niels_to_p1p1(ge_niels_cneg(e, d < 0)));
 #pragma unroll 1
     for (int m = 1; m < 64; m <<= 1) {

@@ -105,9 +105,9 @@ struct DevCtx {
   }
 };
 
-// committees up to this size get per-key combs (528 KB each); larger ones use the cached ladder
+// committees up to this size get per-key combs (5.8 MB each); larger ones use the cached ladder
 #ifndef NWC_COMB_MAX_KEYS
-#define NWC_COMB_MAX_KEYS 4096
+#define NWC_COMB_MAX_KEYS 1024
 #endif
 
 // batches up to this size take the latency kernel (k_verify_comb_wide) on the comb path
@@ -173,8 +173,8 @@ int init_device(DevCtx& d) {
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify_comb), 256, 0));
   d.comb_blocks_per_cu = bpc > 0 ? bpc : 1;
   HIP_TRY(hipMalloc(&d.uc_count, sizeof(uint32_t)));
-  HIP_TRY(hipMalloc(&d.comb_base, nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad)));
-  hipLaunchKernelGGL(nwc::k_build_comb, dim3((unsigned)((nwc::COMB_PER_KEY + 255) / 256)), dim3(256), 0, d.stream,
+  HIP_TRY(hipMalloc(&d.comb_base, nwc::BaseComb::per * sizeof(nwc::ge_niels_pad)));
+  hipLaunchKernelGGL(nwc::k_build_comb<nwc::BaseComb>, dim3((unsigned)((nwc::BaseComb::per + 255) / 256)), dim3(256), 0, d.stream,
                      (const nwc::u32*)nullptr, 1u, d.comb_base);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMalloc(&d.comb16, nwc::COMB16_TOTAL * sizeof(nwc::ge_niels_pad)));
@@ -649,10 +649,10 @@ int nwc_set_committee(const uint8_t* pks, size_t n) {
                        d.cm_tables, d.cm_flags);
     HIP_TRY(hipGetLastError());
     if (n <= NWC_COMB_MAX_KEYS) {
-      // per-key combs for the doubling-free path (528 KB per key)
+      // per-key combs for the doubling-free path (radix 2^12: 5.8 MB per key)
       const size_t entries = n * nwc::COMB_PER_KEY;
       HIP_TRY(hipMalloc(&d.cm_comb, entries * sizeof(nwc::ge_niels_pad)));
-      hipLaunchKernelGGL(nwc::k_build_comb, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, d.stream,
+      hipLaunchKernelGGL(nwc::k_build_comb<nwc::KeyComb>, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, d.stream,
                          d.cm_keys, (nwc::u32)n, d.cm_comb);
       HIP_TRY(hipGetLastError());
     }

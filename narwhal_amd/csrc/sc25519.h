@@ -117,6 +117,35 @@ FE_DEV void sc_recode_radix65536(const u32 s[8], u32 out[8]) {
   }
 }
 
+// Signed radix-2^12 digits of s < 2^253: 22 digits in [-2^11, 2^11), packed as 12-bit fields
+// (d + 2^11), digit w at bits [12 w, 12 w + 12) of out[0..8] (264 bits).
+FE_DEV void sc_recode_radix4096(const u32 s[8], u32 out[9]) {
+  _Pragma("unroll") for (int i = 0; i < 9; ++i) out[i] = 0;
+  i32 carry = 0;
+  _Pragma("unroll") for (int w = 0; w < 22; ++w) {
+    const int b = 12 * w, wi = b >> 5, sh = b & 31;
+    u32 v = s[wi] >> sh;
+    if (sh > 20 && wi + 1 < 8) v |= s[wi + 1] << (32 - sh);
+    i32 d = (i32)(v & 0xFFFu) + carry;
+    carry = (d + 2048) >> 12;
+    d -= carry << 12;
+    const u32 f = (u32)(d + 2048);
+    out[wi] |= f << sh;
+    if (sh > 20) out[wi + 1] |= f >> (32 - sh);
+  }
+}
+// digit w (wave-uniform or per lane) of a radix-2^12 string
+FE_DEV i32 digit4096_at(const u32 d[9], int w) {
+  const int b = 12 * w, wi = b >> 5, sh = b & 31;
+  u32 lo = d[0], hi = d[1];
+  _Pragma("unroll") for (int q = 1; q < 9; ++q) {
+    lo = (q == wi) ? d[q] : lo;
+    hi = (q + 1 < 9 && q == wi) ? d[q + 1] : hi;
+  }
+  const u64 v = ((u64)hi << 32 | lo) >> sh;
+  return (i32)(v & 0xFFFu) - 2048;
+}
+
 // Shift a packed 256-bit digit string left by `bits` (top digits fall out of word 7).
 FE_DEV void digits_shl(u32 d[8], int bits) {
   _Pragma("unroll") for (int i = 7; i > 0; --i) d[i] = (d[i] << bits) | (d[i - 1] >> (32 - bits));
