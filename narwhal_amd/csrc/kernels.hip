@@ -1138,6 +1138,166 @@ __global__ __launch_bounds__(256, 2) void k_sha512_digest32(const uint8_t* __res
   }
 }
 
+// ---- McNaughton-scheduled digests (many long messages) ---------------------------------------
+// k_sha512_digest32 gives each lane one whole message, so a launch of n messages occupies
+// ceil(n / 64) waves and the busiest SIMD runs ceil(n / 64 / SIMDs) of them one after another:
+// at config 4 (100,000 batches, 1,563 waves on 1,024 SIMDs) half the SIMDs run two waves while
+// the rest idle through the second.  Here every SIMD gets exactly one wave (256-thread
+// workgroups, one per CU: the LDS reservation below admits a single workgroup per CU), and wave
+// g owns the messages [g n / G, (g+1) n / G).  Its messages, laid end to end as a tape of
+// compression blocks (S blocks in all, the longest M), are cut into 64 lane segments of
+// T = max(ceil(S / 64), M) blocks; McNaughton's wrap-around rule makes that cut a valid schedule:
+// a message that crosses the boundary between lanes l and l+1 has its FIRST a blocks compressed by
+// lane l+1 at times [0, a) and its remaining blocks by lane l at the END of lane l's segment,
+// which starts no earlier than time a because the message is no longer than T.  Lane l+1 hands
+// the chaining value over through LDS (same wave: the write precedes the read in program order).
+// Every lane prefetches the next block it will compress (and the next message's bounds) one
+// compression ahead, so a single wave per SIMD keeps its VALU busy.
+constexpr uint32_t SHA_NONE = 0xffffffffu;
+struct ShaSchedLds {
+  uint64_t st[4][8][64];     // per wave, per state word, per lane: handed-over chaining values
+  uint32_t chain[4][64];     // per wave, per lane: first message of the lane's segment
+  uint32_t off[4][64];       //                      and the tape offset of the segment in it
+  uint8_t reserve[84 * 1024 - 4 * 8 * 64 * 8 - 2 * 4 * 64 * 4];   // > 80 KiB: one workgroup per CU
+};
+__device__ __forceinline__ uint64_t sha_msg_len(const uint64_t* offsets, const uint64_t* ends, uint64_t i) {
+  return (ends ? ends[i] : offsets[i + 1]) - offsets[i];
+}
+__device__ __forceinline__ uint64_t sha_blocks(uint64_t len) { return (len + 17 + 127) >> 7; }
+
+__global__ __launch_bounds__(256, 1) void k_sha512_digest32_sched(const uint8_t* __restrict__ data,
+                                                                  const uint64_t* __restrict__ offsets,
+                                                                  const uint64_t* __restrict__ ends,
+                                                                  uint64_t n, uint8_t* __restrict__ out32) {
+  __shared__ ShaSchedLds lds;
+  const unsigned wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t G = (uint64_t)gridDim.x * 4, g = (uint64_t)blockIdx.x * 4 + wid;
+  const uint64_t lo = g * n / G;
+  const uint32_t cnt = (uint32_t)((g + 1) * n / G - lo);
+  // tape length S and longest message M of this wave
+  uint64_t S = 0, M = 0;
+  for (uint32_t k = lane; k < cnt; k += 64) {
+    const uint64_t L = sha_blocks(sha_msg_len(offsets, ends, lo + k));
+    S += L;
+    M = L > M ? L : M;
+  }
+  _Pragma("unroll") for (int d = 32; d >= 1; d >>= 1) {
+    S += __shfl_xor(S, d);
+    const uint64_t m2 = __shfl_xor(M, d);
+    M = m2 > M ? m2 : M;
+  }
+  const uint64_t T = (S + 63) / 64 > M ? (S + 63) / 64 : M;
+  // segment starts: message k covers tape [excl, incl); segment l starts at l T
+  lds.chain[wid][lane] = SHA_NONE;
+  lds.off[wid][lane] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  uint64_t carry = 0;
+  for (uint32_t base = 0; base < cnt; base += 64) {
+    const uint32_t k = base + lane;
+    const uint64_t L = k < cnt ? sha_blocks(sha_msg_len(offsets, ends, lo + k)) : 0;
+    uint64_t incl = L;
+    _Pragma("unroll") for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(incl, d);
+      if ((int)lane >= d) incl += y;
+    }
+    incl += carry;
+    const uint64_t excl = incl - L;
+    if (L) {
+      const uint64_t l = (excl + T - 1) / T;
+      if (l < 64 && l * T < incl) {
+        lds.chain[wid][l] = k;
+        lds.off[wid][l] = (uint32_t)(l * T - excl);
+      }
+    }
+    carry = __shfl(incl, 63);
+  }
+  __syncthreads();
+
+  uint32_t k = lds.chain[wid][lane];
+  bool active = k != SHA_NONE;
+  if (!active) k = 0;
+  uint64_t c = lo + k;
+  uint64_t start = 0, len = 0;
+  if (active) { start = offsets[c]; len = sha_msg_len(offsets, ends, c); }
+  uint64_t fast = (start & 15) == 0 ? (len >> 7) : 0;
+  const uint32_t o = lds.off[wid][lane];
+  uint64_t b = 0, e = sha_blocks(len) - o;   // first piece: the message's first blocks
+  bool handoff = o != 0;                     // ... handed to lane - 1 when they end mid-message
+  // bounds of the following message, one piece ahead
+  uint64_t nstart = 0, nlen = 0;
+  if (active && k + 1 < cnt) { nstart = offsets[c + 1]; nlen = sha_msg_len(offsets, ends, c + 1); }
+  uint64_t st[8];
+  sha512_init_state(st);
+  uint4 v[8];
+  if (active && b < fast) {
+    const uint4* q = reinterpret_cast<const uint4*>(data + start);
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] = q[j];
+  }
+#pragma unroll 1
+  for (uint64_t t = 0; t < T; ++t) {
+    uint64_t w[16];
+    if (active) {
+      if (b < fast) {
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) {
+          w[2 * j] = be64_from_le32(v[j].x, v[j].y);
+          w[2 * j + 1] = be64_from_le32(v[j].z, v[j].w);
+        }
+      } else {
+        const ShaBlock r = sha_block_bytes(data + start, len, b);
+        _Pragma("unroll") for (int j = 0; j < 16; ++j) w[j] = r.w[j];
+      }
+    }
+    // where this lane compresses next (index arithmetic only), and its prefetch
+    const bool piece_end = active && b + 1 == e;
+    bool nactive = active, fresh = false;
+    uint64_t nb = b + 1, ne = e, pstart = start, plen = len;
+    if (piece_end) {
+      nactive = k + 1 < cnt && t + 1 < T;
+      const uint64_t tot = sha_blocks(nlen), rem = T - (t + 1);
+      fresh = tot <= rem;
+      nb = fresh ? 0 : tot - rem;   // a message crossing into lane + 1: its last blocks only
+      ne = tot;
+      pstart = nstart;
+      plen = nlen;
+    }
+    const uint64_t pfast = (pstart & 15) == 0 ? (plen >> 7) : 0;
+    if (nactive && nb < pfast) {
+      const uint4* q = reinterpret_cast<const uint4*>(data + pstart) + 8 * nb;
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) v[j] = q[j];
+    }
+    if (active) sha512_compress<true>(st, w);
+    if (piece_end) {
+      if (handoff) {
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) lds.st[wid][j][lane] = st[j];
+      } else {
+        uint32_t* op = reinterpret_cast<uint32_t*>(out32 + 32 * c);
+        _Pragma("unroll") for (int j = 0; j < 4; ++j) {
+          op[2 * j] = __builtin_bswap32((u32)(st[j] >> 32));
+          op[2 * j + 1] = __builtin_bswap32((u32)st[j]);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (nactive) {
+        if (fresh) {
+          sha512_init_state(st);
+        } else {   // lane + 1 compressed this message's first nb blocks at times < t + 1
+          _Pragma("unroll") for (int j = 0; j < 8; ++j) st[j] = lds.st[wid][j][lane + 1];
+        }
+        ++k;
+        ++c;
+        start = nstart;
+        len = nlen;
+        fast = pfast;
+        if (k + 1 < cnt) { nstart = offsets[c + 1]; nlen = sha_msg_len(offsets, ends, c + 1); }
+      }
+      handoff = false;
+    }
+    active = nactive;
+    b = nb;
+    e = ne;
+  }
+}
+
 // ------------------------------------------------------------------------------- keygen + sign
 // Fixed-base scalar multiplication by a reduced scalar (< l) with the LDS base table.
 __device__ __noinline__ ge_p3 base_scalarmult(const u32 a[8], const ge_niels* sB) {

@@ -323,9 +323,31 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   return 0;
 }
 
+// NWC_DIGEST_SCHED=0/1 forces the one-lane-per-message / scheduled digest kernel (A/B and tests).
+int digest_sched_mode() {
+  static const int mode = [] {
+    const char* e = std::getenv("NWC_DIGEST_SCHED");
+    return e ? std::atoi(e) : -1;
+  }();
+  return mode;
+}
+
 int launch_digest(const uint8_t* data, const uint64_t* offsets, const uint64_t* ends, uint64_t n, uint8_t* out32,
                   hipStream_t s) {
   if (n == 0) return 0;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  int cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  // more than one wave per SIMD of one-lane-per-message work: schedule blocks instead
+  const int mode = digest_sched_mode();
+  const bool sched = mode >= 0 ? mode == 1 : n > 64ull * 4 * (uint64_t)cus;
+  if (sched) {
+    hipLaunchKernelGGL(nwc::k_sha512_digest32_sched, dim3((unsigned)cus), dim3(256), 0, s, data, offsets, ends, n,
+                       out32);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   const unsigned grid = (unsigned)((n + 255) / 256);
   hipLaunchKernelGGL(nwc::k_sha512_digest32, dim3(grid), dim3(256), 0, s, data, offsets, ends, n, out32);
   HIP_TRY(hipGetLastError());

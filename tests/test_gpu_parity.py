@@ -72,6 +72,56 @@ def test_digest_random_lengths_vs_hashlib(lib):
         assert g.to_vec() == hashlib.sha512(m).digest()[:32], len(m)
 
 
+def _sched_count(torch):
+    """Messages per launch above which launch_digest takes the McNaughton-scheduled kernel."""
+    return 64 * 4 * torch.cuda.get_device_properties(0).multi_processor_count
+
+
+def test_digest_scheduled_ragged_vs_hashlib(lib, torch_dev):
+    """k_sha512_digest32_sched: > one wave per SIMD of ragged messages (short, long, empty,
+    unaligned), so lane segments cut messages and hand chaining values over between lanes."""
+    torch = torch_dev
+    from narwhal_amd import device
+    rng = np.random.default_rng(21)
+    n = _sched_count(torch) + 4321
+    lens = rng.integers(0, 2500, n)
+    lens[rng.integers(0, n, 40)] = rng.integers(20_000, 300_000, 40)   # a few long ones set T
+    lens[rng.integers(0, n, 200)] = 0
+    blob = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    data = torch.from_numpy(blob).cuda()
+    out = device.sha512_trunc32(data, torch.from_numpy(offs).cuda())
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    raw = blob.tobytes()
+    bad = [i for i in range(n) if o[i].tobytes() != hashlib.sha512(raw[offs[i]:offs[i + 1]]).digest()[:32]]
+    assert not bad, (len(bad), bad[:10])
+
+
+def test_digest_scheduled_cfg4_shape(lib, torch_dev):
+    """Config-4 shape through the scheduled kernel: > one wave per SIMD of 508,052-B batches
+    (a pool of 48 distinct aligned batches cycled by range), every digest checked."""
+    torch = torch_dev
+    import make_golden
+    from narwhal_amd import device
+    pool = 48
+    batches = [make_golden.cfg4_batch(i) for i in range(pool)]
+    stride = (len(batches[0]) + 255) & ~255
+    blob = np.zeros(stride * pool, dtype=np.uint8)
+    for i, b in enumerate(batches):
+        blob[i * stride:i * stride + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    want = [hashlib.sha512(b).digest()[:32] for b in batches]
+    n = _sched_count(torch) + 1000
+    idx = (np.arange(n) * 7) % pool
+    starts = torch.from_numpy((idx * stride).astype(np.int64)).cuda()
+    ends = starts + len(batches[0])
+    out = device.sha512_trunc32_ranges(torch.from_numpy(blob).cuda(), starts, ends)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    bad = [i for i in range(n) if o[i].tobytes() != want[idx[i]]]
+    assert not bad, (len(bad), bad[:10])
+
+
 def test_digest_device_resident_unaligned(lib, torch_dev):
     """nwc_dev_sha512_trunc32 on contiguous (unaligned) offsets, the reference's own layout."""
     torch = torch_dev
