@@ -131,17 +131,28 @@ __device__ __forceinline__ void sha512_init_state(uint64_t st[8]) {
 // ASM = true (the digest kernel): opaque 64-bit adds, -18 % instructions per block.  The verify
 // kernels keep plain adds (ASM = false): their one challenge block is ~1 % of a verification,
 // and the opaque adds cost them registers (more spills in the prologue).
+// The digest kernels (ASM = true) run one wave per SIMD, where every scalar instruction takes an
+// issue slot of its own: they fetch a pass's 16 round constants into SGPRs once per pass (two
+// s_load_dwordx16 and one wait) instead of an address computation, a load and a wait per round.
+template <bool ASM> __device__ __forceinline__ void sha_pass_constants(int pass, uint64_t k[16]) {
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) k[j] = SHA512_K[16 * pass + j];
+  if constexpr (ASM) {
+    _Pragma("unroll") for (int j = 0; j < 16; ++j) asm volatile("" : "+s"(k[j]));
+  }
+}
 template <bool ASM = false> __device__ __forceinline__ void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
   {
     constexpr bool SCHED = false;   // rounds 0..15 use the message words as they are
-    const uint64_t* k = SHA512_K;
+    uint64_t k[16];
+    sha_pass_constants<ASM>(0, k);
     NWC_SHA_16ROUNDS
   }
 #pragma unroll 1
   for (int pass = 1; pass < 5; ++pass) {
     constexpr bool SCHED = true;
-    const uint64_t* k = SHA512_K + 16 * pass;
+    uint64_t k[16];
+    sha_pass_constants<ASM>(pass, k);
     NWC_SHA_16ROUNDS
   }
 #undef NWC_SHA_16ROUNDS
