@@ -496,8 +496,30 @@ def cpu_baseline_digest(budget_s: float):
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": reps * len(blob) / dt / 1e9, "unit": "GB/s", "cores": th, "kind": "port",
-            "sample": "%d x %d cfg-4 batches (C restatement SHA-512, %d threads, %.1f s)" % (reps, nb, th, dt)}
+    out = {"value": reps * len(blob) / dt / 1e9, "unit": "GB/s", "cores": th, "kind": "port",
+           "sample": "%d x %d cfg-4 batches (C restatement SHA-512, %d threads, %.1f s)" % (reps, nb, th, dt)}
+    out["openssl"] = cpu_digest_openssl(blob, nb, th, budget_s / 2)
+    return out
+
+
+def cpu_digest_openssl(blob: bytes, nb: int, th: int, budget_s: float):
+    """SURVEY.md §8(d)'s digest baseline: OpenSSL SHA-512 (hashlib, which releases the GIL on
+    large inputs) over the same cfg-4 batches on `th` host threads, one batch per call."""
+    from concurrent.futures import ThreadPoolExecutor
+    mv = memoryview(blob)
+    views = [mv[b * CFG4_BATCH_BYTES:(b + 1) * CFG4_BATCH_BYTES] for b in range(nb)]
+    ok = hashlib.sha512(views[0]).digest()[:32] == hashlib.sha512(cfg4_host_batch(0)).digest()[:32]
+    with ThreadPoolExecutor(th) as ex:
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            list(ex.map(lambda v: hashlib.sha512(v).digest()[:32], views))
+            reps += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+        dt = time.perf_counter() - t0
+    return {"value": reps * nb * CFG4_BATCH_BYTES / dt / 1e9, "unit": "GB/s", "cores": th, "kind": "openssl",
+            "parity_ok": ok, "sample": "%d x %d cfg-4 batches (hashlib/OpenSSL SHA-512, %d threads, %.1f s)" % (reps, nb, th, dt)}
 
 
 # ---- main ------------------------------------------------------------------------------------
