@@ -162,7 +162,7 @@ def cfg4_host_batch(b: int) -> bytes:
     return bytes(out)
 
 
-def bench_cfg1(lib, calls: int = 2000):
+def bench_cfg1(lib, calls: int = 10000, cpu_baseline: bool = False):
     """BASELINE config 1: Signature::verify_batch on a 4-node certificate (3 votes, 32-byte
     digest) through the host ABI (H2D + kernel + D2H per call).  Latency-bound by design.
     Timed without and with the committee cache (the 4 authorities' keys, as a node always has
@@ -194,7 +194,29 @@ def bench_cfg1(lib, calls: int = 2000):
         lat = np.array(lat) * 1e6
         out[tag] = {"calls": calls, "p50_us": float(np.percentile(lat, 50)),
                     "p99_us": float(np.percentile(lat, 99)), "calls_per_s": float(1e6 / lat.mean())}
+    if cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_cfg1(d, p, s, n, min(calls, 2000))
     return out
+
+
+def cpu_baseline_cfg1(d: bytes, p: bytes, s: bytes, n: int, calls: int):
+    """The same 3-vote verify_batch on one host core with the dalek algorithm (random z_i +
+    Straus MSM; oracle/nwc_oracle.c orc_verify_batch_straus), per-call latency as on the GPU."""
+    import ctypes
+    from tests.oracle_lib import load_oracle
+    orc = load_oracle().lib
+    bd, bp, bs = (ctypes.create_string_buffer(x, len(x)) for x in (d, p, s))
+    lat = []
+    for i in range(calls + 20):
+        t0 = time.perf_counter()
+        rc = orc.orc_verify_batch_straus(bd, bp, bs, n, i + 1)
+        dt = time.perf_counter() - t0
+        assert rc == 1, rc   # 1 = Ok (all valid)
+        if i >= 20:
+            lat.append(dt)
+    lat = np.array(lat) * 1e6
+    return {"p50_us": float(np.percentile(lat, 50)), "p99_us": float(np.percentile(lat, 99)), "cores": 1,
+            "kind": "port", "sample": "%d calls, C restatement of dalek verify_batch (Straus), 1 thread" % calls}
 
 
 def cpu_baseline_cfg3(cdig, pks, sigs, m: int, Q: int, bad, budget_s: float):
@@ -534,7 +556,7 @@ def main():
     ap.add_argument("--digest-steps", type=int, default=1)
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds per CPU-baseline leg (0 = skip)")
     ap.add_argument("--cfg3-certs", type=int, default=100000, help="config 3 certificates (0 = skip)")
-    ap.add_argument("--cfg1-calls", type=int, default=2000, help="config 1 latency calls (0 = skip)")
+    ap.add_argument("--cfg1-calls", type=int, default=10000, help="config 1 latency calls (0 = skip)")
     ap.add_argument("--wire-certs", type=int, default=20000, help="cfg 3 from wire bytes (0 = skip)")
     ap.add_argument("--cfg5-total", type=int, default=64 << 20, help="cfg 5 signatures over all ranks (0 = skip)")
     args = ap.parse_args()
@@ -613,7 +635,7 @@ def main():
         extras["cfg3"] = bench_cfg3(lib, args.cfg3_certs, max(1, args.steps // 2),
                                     args.cpu_budget / 2 if rank == 0 else 0.0)
     if world == 1 and args.cfg1_calls > 0:
-        extras["cfg1"] = bench_cfg1(lib, args.cfg1_calls)
+        extras["cfg1"] = bench_cfg1(lib, args.cfg1_calls, cpu_baseline=args.cpu_budget > 0)
     if world == 1 and args.wire_certs > 0:
         extras["cfg3_wire"] = bench_cfg3_wire(lib, args.wire_certs, max(1, args.steps // 2))
 
