@@ -199,13 +199,17 @@ __global__ void k_build_key_tables(const u32* __restrict__ keys, u32 n, ge_niels
 //   BaseComb: P = B, radix 2^8, 32 windows (528 KB, nwc_init) -- the latency kernel's basepoint
 //   KeyComb:  P = -A_key, radix 2^12, 22 windows (5.8 MB per key, nwc_set_committee)
 // One lane per entry: BITS*w doublings of P, a BITS-bit double-and-add, one inversion.
+#ifndef NWC_KEY_COMB_BITS
+#define NWC_KEY_COMB_BITS 12
+#define NWC_KEY_COMB_WINDOWS 22
+#endif
 template <int BITS, int WINDOWS>
 struct CombShape {
   static constexpr int bits = BITS, windows = WINDOWS, entries = (1 << (BITS - 1)) + 1;
   static constexpr size_t per = (size_t)WINDOWS * entries;
 };
 using BaseComb = CombShape<8, 32>;
-using KeyComb = CombShape<12, 22>;
+using KeyComb = CombShape<NWC_KEY_COMB_BITS, NWC_KEY_COMB_WINDOWS>;
 constexpr size_t COMB_PER_KEY = KeyComb::per;
 template <class S>
 __global__ void k_build_comb(const u32* __restrict__ keys, u32 n, ge_niels_pad* __restrict__ out) {
@@ -885,16 +889,16 @@ __device__ __forceinline__ i32 next_digit16(u32 d[8]) {
   digits_shl(d, 16);
   return v;
 }
-constexpr int COMB_SUM_ADDS = KeyComb::windows + COMB16_WINDOWS;   // 38
+constexpr int COMB_SUM_ADDS = KeyComb::windows + COMB16_WINDOWS;   // 38 (radix 2^12)
 __device__ __forceinline__ ge_p2 comb_sum(const u32 sw[8], const u32 kw[8], const ge_niels_pad* TB16,
                                           const ge_niels_pad* TA) {
   u32 sd[8], kd[9];
   sc_recode_radix65536(sw, sd);
-  sc_recode_radix4096(kw, kd);
-  i32 d = digit4096_at(kd, KeyComb::windows - 1);
+  sc_recode_radix<KeyComb::bits, KeyComb::windows>(kw, kd);
+  i32 d = digit_at<KeyComb::bits>(kd, KeyComb::windows - 1);
   ge_niels e = comb_load(TA, KeyComb::entries, KeyComb::windows - 1, d);
   ge_p1p1 t = ge_niels_to_p1p1(ge_niels_cneg(e, d < 0));
-  i32 dn = digit4096_at(kd, KeyComb::windows - 2);
+  i32 dn = digit_at<KeyComb::bits>(kd, KeyComb::windows - 2);
   ge_niels en = comb_load(TA, KeyComb::entries, KeyComb::windows - 2, dn);
 #pragma unroll 1
   for (int i = 1; i < COMB_SUM_ADDS; ++i) {
@@ -902,7 +906,7 @@ __device__ __forceinline__ ge_p2 comb_sum(const u32 sw[8], const u32 kw[8], cons
     d = dn;
     const int nx = i + 1;   // entry to fetch: key window 21 - nx, or B window 37 - nx
     if (nx < KeyComb::windows) {
-      dn = digit4096_at(kd, KeyComb::windows - 1 - nx);
+      dn = digit_at<KeyComb::bits>(kd, KeyComb::windows - 1 - nx);
       en = comb_load(TA, KeyComb::entries, KeyComb::windows - 1 - nx, dn);
     } else if (nx < COMB_SUM_ADDS) {
       dn = next_digit16(sd);
@@ -1026,10 +1030,10 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
     u32 kw[8], sd[8], kd[9];
     challenge(rw, aw, mw, kw);
     sc_recode_radix256(sw, sd);
-    sc_recode_radix4096(kw, kd);
+    sc_recode_radix<KeyComb::bits, KeyComb::windows>(kw, kd);
     const bool bside = lane < 32;
     const int w = bside ? lane : min(lane - 32, KeyComb::windows - 1);
-    const i32 d = bside ? digit256_at(sd, w) : digit4096_at(kd, w);
+    const i32 d = bside ? digit256_at(sd, w) : digit_at<KeyComb::bits>(kd, w);
     ge_niels e = bside ? comb_load(ca.comb_base, BaseComb::entries, w, d)
                        : comb_load(cm.comb + (size_t)kk * COMB_PER_KEY, KeyComb::entries, w, d);
     if (lane >= 32 + KeyComb::windows) e = ge_niels_identity();

@@ -117,34 +117,39 @@ FE_DEV void sc_recode_radix65536(const u32 s[8], u32 out[8]) {
   }
 }
 
-// Signed radix-2^12 digits of s < 2^253: 22 digits in [-2^11, 2^11), packed as 12-bit fields
-// (d + 2^11), digit w at bits [12 w, 12 w + 12) of out[0..8] (264 bits).
-FE_DEV void sc_recode_radix4096(const u32 s[8], u32 out[9]) {
+// Signed radix-2^BITS digits of s < 2^253 (BITS <= 16): WINDOWS digits in [-2^(BITS-1), 2^(BITS-1)),
+// packed as BITS-bit fields (d + 2^(BITS-1)), digit w at bits [BITS w, BITS w + BITS) of out[0..8].
+template <int BITS, int WINDOWS>
+FE_DEV void sc_recode_radix(const u32 s[8], u32 out[9]) {
+  static_assert(BITS * WINDOWS <= 288 && BITS * WINDOWS >= 254, "digit string");
   _Pragma("unroll") for (int i = 0; i < 9; ++i) out[i] = 0;
   i32 carry = 0;
-  _Pragma("unroll") for (int w = 0; w < 22; ++w) {
-    const int b = 12 * w, wi = b >> 5, sh = b & 31;
-    u32 v = s[wi] >> sh;
-    if (sh > 20 && wi + 1 < 8) v |= s[wi + 1] << (32 - sh);
-    i32 d = (i32)(v & 0xFFFu) + carry;
-    carry = (d + 2048) >> 12;
-    d -= carry << 12;
-    const u32 f = (u32)(d + 2048);
+  _Pragma("unroll") for (int w = 0; w < WINDOWS; ++w) {
+    const int b = BITS * w, wi = b >> 5, sh = b & 31;
+    u32 v = wi < 8 ? s[wi] >> sh : 0u;
+    if (sh > 32 - BITS && wi + 1 < 8) v |= s[wi + 1] << (32 - sh);
+    i32 d = (i32)(v & ((1u << BITS) - 1u)) + carry;
+    carry = (d + (1 << (BITS - 1))) >> BITS;
+    d -= carry << BITS;
+    const u32 f = (u32)(d + (1 << (BITS - 1)));
     out[wi] |= f << sh;
-    if (sh > 20) out[wi + 1] |= f >> (32 - sh);
+    if (sh > 32 - BITS) out[wi + 1] |= f >> (32 - sh);
   }
 }
-// digit w (wave-uniform or per lane) of a radix-2^12 string
-FE_DEV i32 digit4096_at(const u32 d[9], int w) {
-  const int b = 12 * w, wi = b >> 5, sh = b & 31;
+// digit w (wave-uniform or per lane) of a radix-2^BITS string
+template <int BITS>
+FE_DEV i32 digit_at(const u32 d[9], int w) {
+  const int b = BITS * w, wi = b >> 5, sh = b & 31;
   u32 lo = d[0], hi = d[1];
   _Pragma("unroll") for (int q = 1; q < 9; ++q) {
     lo = (q == wi) ? d[q] : lo;
     hi = (q + 1 < 9 && q == wi) ? d[q + 1] : hi;
   }
   const u64 v = ((u64)hi << 32 | lo) >> sh;
-  return (i32)(v & 0xFFFu) - 2048;
+  return (i32)(v & ((1u << BITS) - 1u)) - (1 << (BITS - 1));
 }
+FE_DEV void sc_recode_radix4096(const u32 s[8], u32 out[9]) { sc_recode_radix<12, 22>(s, out); }
+FE_DEV i32 digit4096_at(const u32 d[9], int w) { return digit_at<12>(d, w); }
 
 // Shift a packed 256-bit digit string left by `bits` (top digits fall out of word 7).
 FE_DEV void digits_shl(u32 d[8], int bits) {
