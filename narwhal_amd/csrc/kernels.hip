@@ -850,7 +850,10 @@ __global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {
 // Equations whose key is not cached go to uc_list and are verified by k_verify in list mode.
 struct CombRec { fe X, Y, Z, P; u32 yr[8]; u32 meta; u32 pad[3]; };
 static_assert(sizeof(CombRec) == 208, "comb record layout");
-constexpr int COMB_BATCH = 16;
+#ifndef NWC_COMB_BATCH
+#define NWC_COMB_BATCH 64
+#endif
+constexpr int COMB_BATCH = NWC_COMB_BATCH;
 constexpr size_t COMB_REC_U4 = sizeof(CombRec) / 16;
 constexpr size_t COMB_BYTES_PER_LANE = COMB_BATCH * sizeof(CombRec);
 
@@ -861,14 +864,17 @@ __device__ __forceinline__ ge_niels comb_load(const ge_niels_pad* tab, int entri
   _Pragma("unroll") for (int c = 0; c < 8; ++c) e.u[c] = q[c];
   return e.p.n;
 }
-__device__ __forceinline__ void rec_store(uint4* base, int j, const CombRec& r) {
+// Records are lane-interleaved: uint4 c of record j of lane slot l sits at
+// scratch[(j * COMB_REC_U4 + c) * lanes + l], so each of a wave's 13 record stores/loads moves one
+// contiguous KB (lanes = the persistent grid's lane count).
+__device__ __forceinline__ void rec_store(uint4* base, size_t lanes, int j, const CombRec& r) {
   const uint4* src = reinterpret_cast<const uint4*>(&r);
-  _Pragma("unroll") for (size_t c = 0; c < COMB_REC_U4; ++c) base[j * COMB_REC_U4 + c] = src[c];
+  _Pragma("unroll") for (size_t c = 0; c < COMB_REC_U4; ++c) base[(j * COMB_REC_U4 + c) * lanes] = src[c];
 }
-__device__ __forceinline__ CombRec rec_load(const uint4* base, int j) {
+__device__ __forceinline__ CombRec rec_load(const uint4* base, size_t lanes, int j) {
   CombRec r;
   uint4* dst = reinterpret_cast<uint4*>(&r);
-  _Pragma("unroll") for (size_t c = 0; c < COMB_REC_U4; ++c) dst[c] = base[j * COMB_REC_U4 + c];
+  _Pragma("unroll") for (size_t c = 0; c < COMB_REC_U4; ++c) dst[c] = base[(j * COMB_REC_U4 + c) * lanes];
   return r;
 }
 // affine Niels entry as a completed point (2x : 2y : 2 : 2) -- starts the sum without an add
@@ -919,7 +925,8 @@ __device__ __forceinline__ ge_p2 comb_sum(const u32 sw[8], const u32 kw[8], cons
 
 __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs ca) {
   const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint4* recs = reinterpret_cast<uint4*>(a.scratch + slot * COMB_BYTES_PER_LANE);
+  uint4* recs = reinterpret_cast<uint4*>(a.scratch) + slot;
+  const size_t lanes = (size_t)gridDim.x * blockDim.x;
   const Committee& cm = a.committee;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x; c0 < a.n; c0 += stride * COMB_BATCH) {
@@ -953,7 +960,7 @@ __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs c
       r.X = q.X; r.Y = q.Y; r.Z = fe_select(q.Z, fe_one(), zbad); r.P = P;
       r.meta = (ok && !zbad ? 1u : 0u) | ((rw[7] >> 31) << 1);
       r.pad[0] = r.pad[1] = r.pad[2] = 0;
-      rec_store(recs, j, r);
+      rec_store(recs, lanes, j, r);
       P = fe_mul(P, r.Z);
       nb = j + 1;
     }
@@ -961,7 +968,7 @@ __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs c
     fe inv = fe_invert(P);
 #pragma unroll 1
     for (int j = nb - 1; j >= 0; --j) {
-      const CombRec r = rec_load(recs, j);
+      const CombRec r = rec_load(recs, lanes, j);
       const fe zi = fe_mul(inv, r.P);
       inv = fe_mul(inv, r.Z);
       u32 yw[8], xw[8];
