@@ -114,6 +114,10 @@ struct DevCtx {
 #ifndef NWC_PINNED_STAGE_MAX
 #define NWC_PINNED_STAGE_MAX (1u << 20)
 #endif
+// persistent verify grid: this many blocks per resident block slot
+#ifndef NWC_VERIFY_GRID_MULT
+#define NWC_VERIFY_GRID_MULT 8
+#endif
 #ifndef NWC_WIDE_MAX
 #define NWC_WIDE_MAX 1024
 #endif
@@ -266,7 +270,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   }
   const uint64_t tiles = (n + 255) / 256;
   // persistent grid: a few blocks per resident slot so the tail is short
-  const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * 4;
+  const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * NWC_VERIFY_GRID_MULT;
   const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
   size_t need = (size_t)cap * 256 * 2 * nwc::TAB_BYTES_PER_LANE;
   // comb grid: at most the resident blocks; tile t goes to block t mod grid, so every lane gets
