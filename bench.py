@@ -88,11 +88,21 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("WORLD_SIZE=%d but --gpus %d (launch N>1 with torch.distributed.run)" % (world, args.gpus))
+    # NWC_BENCH_BACKEND=gloo rehearses the N>1 code path with more ranks than GPUs (ranks share
+    # devices round-robin); the driver's runs use the default, RCCL with one GPU per rank.
+    backend = os.environ.get("NWC_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > ndev:
+        raise SystemExit("WORLD_SIZE=%d but only %d GPUs visible" % (world, ndev))
+    local = local % max(1, ndev)
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return rank, world, local
 
 
