@@ -560,7 +560,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1 << 20, help="triples per GPU (cfg 2: 1M)")
+    ap.add_argument("--triples", "--n", dest="n", type=int, default=1 << 20,
+                    help="triples per GPU (cfg 2: 1M); under torch.distributed.run spell it --triples")
     ap.add_argument("--digest-batches", type=int, default=100000, help="cfg 4: 100k batches (0 = skip)")
     ap.add_argument("--digest-pool", type=int, default=16384, help="distinct batches resident in HBM")
     ap.add_argument("--digest-steps", type=int, default=1)

@@ -22,5 +22,5 @@ $P --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_A
 $P --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py $ARGS > $OUT/pmc_fetch.log 2>&1
 $P --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py $ARGS > $OUT/pmc_write.log 2>&1
 $P --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT/pmc_clk -o run -- python3 $R/bench.py $ARGS > $OUT/pmc_clk.log 2>&1
-$P --kernel-trace --stats --output-format csv -d $OUT/trace_cfg3 -o run -- python3 $R/bench.py --steps 2 --warmup 1 --cpu-budget 0 --cfg1-calls 0 --n 65536 --digest-batches 0 --cfg5-total 0 > $OUT/trace_cfg3.log 2>&1
+$P --kernel-trace --stats --output-format csv -d $OUT/trace_cfg3 -o run -- python3 $R/bench.py --steps 2 --warmup 1 --cpu-budget 0 --cfg1-calls 0 --triples 65536 --digest-batches 0 --cfg5-total 0 > $OUT/trace_cfg3.log 2>&1
 echo done
