@@ -167,6 +167,31 @@ __device__ __forceinline__ int committee_lookup(const Committee& c, const u32 aw
   return found;
 }
 
+// l * P != O: P has a non-zero 8-torsion component.  dalek's verify_batch scales A_i by
+// (z_i k_i mod l), so a key with torsion puts its vote in the randomized domain (SURVEY.md A.4 as
+// corrected in round 2; oracle/nwc_oracle.c orc_vote_class).  l = 2^252 + c0 (c0 < 2^125):
+// left-to-right double-and-add, 252 doublings and 61 cached additions.  Used once per committee
+// key and once per distinct uncached key of a batch-leaf launch, so it is not on the hot path.
+__device__ __noinline__ bool ge_has_torsion(const ge_p3& P) {
+  const ge_cached pc = ge_p3_to_cached(P);
+  ge_p2 acc = ge_p3_to_p2(P);   // bit 252
+#pragma unroll 1
+  for (int bit = 251; bit >= 0; --bit) {
+    ge_p1p1 t = ge_p2_dbl(acc);
+    if ((SC_L[bit >> 5] >> (bit & 31)) & 1u) t = ge_add_cached(ge_p1p1_to_p3(t), pc);
+    acc = ge_p1p1_to_p2(t);
+  }
+  return !(fe_is_zero(acc.X) && fe_is_zero(fe_sub(acc.Y, acc.Z)));
+}
+
+// Committee key flags: bit0 = decodes, bit1 = small-order, bit2 = has an 8-torsion component.
+constexpr u32 KEY_DECODES = 1u, KEY_SMALL_ORDER = 2u, KEY_TORSION = 4u;
+// Verdict flags of a cached key for the equation mode: strict rejects small-order A (A.3 step 3),
+// the batch leaf rejects torsion-bearing A (randomized domain, answered Err).
+__device__ __forceinline__ bool key_flags_ok(u32 fl, bool strict) {
+  return (fl & KEY_DECODES) && !(fl & (strict ? KEY_SMALL_ORDER : KEY_TORSION));
+}
+
 // One lane per (key, j): table[key][j] = j * (-A_key); lane j == 0 also writes the flags.
 __global__ void k_build_key_tables(const u32* __restrict__ keys, u32 n, ge_niels* __restrict__ tables,
                                    u32* __restrict__ flags) {
@@ -188,7 +213,9 @@ __global__ void k_build_key_tables(const u32* __restrict__ keys, u32 n, ge_niels
     if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, nc));
   }
   tables[(size_t)key * 129 + j] = ge_p3_to_niels(acc);
-  if (j == 0) flags[key] = (ok[0] ? 1u : 0u) | (ycanon_is_small_order(yc[0]) ? 2u : 0u);
+  if (j == 0)
+    flags[key] = (ok[0] ? KEY_DECODES : 0u) | (ycanon_is_small_order(yc[0]) ? KEY_SMALL_ORDER : 0u) |
+                 (ok[0] && ge_has_torsion(A[0]) ? KEY_TORSION : 0u);
 }
 
 // ------------------------------------------------------------------------------- committee combs
@@ -693,8 +720,8 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
     bool r_ok[1];
     decompress_one(R, rw, yr, r_ok);
     const u32 fl = cm.flags[key];
-    const bool small = strict && (((fl >> 1) & 1) || ycanon_is_small_order(yr[0]));
-    const bool ok = s_ok && (fl & 1) && r_ok[0] && !small;
+    const bool small = strict && ycanon_is_small_order(yr[0]);
+    const bool ok = s_ok && key_flags_ok(fl, strict) && r_ok[0] && !small;
     u32 kw[8];
     challenge(rw, aw, mw, kw);
     const lat::HalfScalars h = lat::reduce(kw);
@@ -837,6 +864,96 @@ __global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------- torsion of batch-leaf keys
+// Batch-leaf equations (strict == 0) whose key is NOT in the committee cache have passed e == O
+// without the key's torsion test.  A launch of n equations dedupes the keys of the equations that
+// passed in a per-launch hash set (k_tors_mark; cached keys instead use their KEY_TORSION flag
+// directly), tests each distinct key once (k_tors_eval: ge_has_torsion), and clears the verdict bit
+// of every equation whose key has torsion (k_tors_apply).  Committees repeat keys, so the distinct
+// count -- and the cost -- is the committee size, not the vote count.
+struct TorsArgs {
+  const uint8_t* pks;
+  uint64_t* bits;           // the launch's verdict words
+  const uint32_t* list;     // nullptr: equations 0 .. n-1; else list[0 .. *count)
+  const uint32_t* count;
+  uint64_t n;
+  int32_t* slots;           // hash set: representative equation index, -1 = empty
+  uint32_t slot_mask;
+  uint32_t* uniq;           // slots that hold a distinct key
+  uint32_t* nuniq;
+  uint32_t* tflag;          // per slot: 1 = the key has torsion
+  Committee committee;
+};
+__device__ __forceinline__ bool tors_candidate(const TorsArgs& t, uint64_t idx, uint64_t& i, u32 aw[8], int& key) {
+  i = t.list ? (uint64_t)t.list[idx] : idx;
+  if (!((t.bits[i >> 6] >> (i & 63)) & 1)) return false;
+  load_words8(t.pks + 32 * i, aw);
+  key = committee_lookup(t.committee, aw);
+  return true;
+}
+__device__ __forceinline__ bool tors_key_eq(const uint8_t* pks, int32_t rep, const u32 aw[8]) {
+  u32 w[8];
+  load_words8(pks + 32 * (uint64_t)rep, w);
+  u32 d = 0;
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) d |= w[k] ^ aw[k];
+  return d == 0;
+}
+__global__ __launch_bounds__(256) void k_tors_mark(TorsArgs t) {
+  const uint64_t N = t.list ? (uint64_t)*t.count : t.n;
+  for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < N; idx += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t i;
+    u32 aw[8];
+    int key;
+    if (!tors_candidate(t, idx, i, aw, key)) continue;
+    if (key >= 0) {
+      if (t.committee.flags[key] & KEY_TORSION)
+        atomicAnd(reinterpret_cast<unsigned long long*>(t.bits) + (i >> 6), ~(1ull << (i & 63)));
+      continue;
+    }
+    u32 h = committee_hash(aw[0], aw[1]) & t.slot_mask;
+    for (;;) {   // the set holds at most half its slots: the probe ends
+      int32_t cur = t.slots[h];
+      if (cur < 0) {
+        cur = atomicCAS(&t.slots[h], -1, (int32_t)i);
+        if (cur < 0) { t.uniq[atomicAdd(t.nuniq, 1u)] = h; break; }
+      }
+      if (tors_key_eq(t.pks, cur, aw)) break;
+      h = (h + 1) & t.slot_mask;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_tors_eval(TorsArgs t) {
+  const uint32_t N = *t.nuniq;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x) {
+    const uint32_t h = t.uniq[j];
+    u32 aw[8];
+    load_words8(t.pks + 32 * (uint64_t)t.slots[h], aw);
+    ge_p3 A[1];
+    u32 yc[1][8];
+    bool ok[1];
+    decompress_one(A, aw, yc, ok);
+    t.tflag[h] = (ok[0] && ge_has_torsion(A[0])) ? 1u : 0u;
+  }
+}
+__global__ __launch_bounds__(256) void k_tors_apply(TorsArgs t) {
+  const uint64_t N = t.list ? (uint64_t)*t.count : t.n;
+  for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < N; idx += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t i;
+    u32 aw[8];
+    int key;
+    if (!tors_candidate(t, idx, i, aw, key) || key >= 0) continue;
+    // k_tors_mark inserted the key at or before the first empty slot of its probe sequence
+    u32 h = committee_hash(aw[0], aw[1]) & t.slot_mask;
+    int32_t rep = t.slots[h];
+    while (rep >= 0 && !tors_key_eq(t.pks, rep, aw)) {
+      h = (h + 1) & t.slot_mask;
+      rep = t.slots[h];
+    }
+    // (rep < 0 cannot happen; clearing the bit then errs on the side of Err)
+    if (rep < 0 || t.tflag[h]) atomicAnd(reinterpret_cast<unsigned long long*>(t.bits) + (i >> 6), ~(1ull << (i & 63)));
+  }
+}
+
 // ------------------------------------------------------------------------------- committee comb verify
 // Doubling-free verification for equations whose key is in the committee cache:
 //   R' = s B + k (-A) = sum_w combB[w][s_w] + sum_w combA_key[w][k_w]      (64 Niels adds)
@@ -949,8 +1066,8 @@ __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs c
       CombRec r;
       fe_to_words(fe_from_words(rw), r.yr);   // y_R mod p
       const u32 fl = cm.flags[kk];
-      const bool small = a.strict && (((fl >> 1) & 1) || ycanon_is_small_order(r.yr));
-      const bool ok = active && key >= 0 && sc_lt_l(sw) && (fl & 1) && !small;
+      const bool small = a.strict && ycanon_is_small_order(r.yr);
+      const bool ok = active && key >= 0 && sc_lt_l(sw) && key_flags_ok(fl, a.strict != 0) && !small;
       u32 kw[8];
       challenge(rw, aw, mw, kw);
       const ge_p2 q = comb_sum(sw, kw, ca.comb16, cm.comb + (size_t)kk * COMB_PER_KEY);
@@ -1054,7 +1171,7 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
   __syncthreads();
   if (threadIdx.x == 0) {
     const u32 fl = cm.flags[kk];
-    const bool flags_ok = key >= 0 && sc_lt_l(sw) && (fl & 1) && !(a.strict && ((fl >> 1) & 1)) && sh_rok;
+    const bool flags_ok = key >= 0 && sc_lt_l(sw) && key_flags_ok(fl, a.strict != 0) && sh_rok;
     const bool eq = fe_is_zero(fe_sub(sum.X, fe_mul(sh_rx, sum.Z))) && fe_is_zero(fe_sub(sum.Y, fe_mul(sh_ry, sum.Z)));
     if (key < 0) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;
     if (flags_ok && eq) atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));

@@ -67,6 +67,12 @@ struct DevCtx {
   uint32_t* fb_count = nullptr;
   size_t fb_cap = 0;
   hipEvent_t scratch_free = nullptr;
+  // batch-leaf torsion post-pass (k_tors_*): key hash set sized for fb_cap equations
+  int32_t* ts_slots = nullptr;
+  uint32_t* ts_flag = nullptr;
+  uint32_t* ts_uniq = nullptr;
+  uint32_t* ts_nuniq = nullptr;
+  uint32_t ts_slot_count = 0;
   // committee key cache (nwc_set_committee); buffers replaced only after scratch_free
   nwc::u32* cm_keys = nullptr;
   nwc::u32* cm_flags = nullptr;
@@ -236,14 +242,51 @@ int ensure_scratch(DevCtx& d, size_t bytes, uint64_t n) {
   if (n > d.fb_cap) {
     if (d.fb_list) HIP_TRY(hipFree(d.fb_list));
     if (d.uc_list) HIP_TRY(hipFree(d.uc_list));
+    if (d.ts_slots) HIP_TRY(hipFree(d.ts_slots));
+    if (d.ts_flag) HIP_TRY(hipFree(d.ts_flag));
+    if (d.ts_uniq) HIP_TRY(hipFree(d.ts_uniq));
     d.fb_list = nullptr;
     d.uc_list = nullptr;
+    d.ts_slots = nullptr;
+    d.ts_flag = nullptr;
+    d.ts_uniq = nullptr;
     d.fb_cap = 0;
+    d.ts_slot_count = 0;
     const size_t c = n + n / 2 + 4096;
     HIP_TRY(hipMalloc(&d.fb_list, 4 * c));
     HIP_TRY(hipMalloc(&d.uc_list, 4 * c));
+    // the hash set stays at most half full: >= 2 slots per equation
+    uint32_t slots = 1024;
+    while (slots < 2 * c) slots <<= 1;
+    HIP_TRY(hipMalloc(&d.ts_slots, 4 * (size_t)slots));
+    HIP_TRY(hipMalloc(&d.ts_flag, 4 * (size_t)slots));
+    HIP_TRY(hipMalloc(&d.ts_uniq, 4 * c));
+    d.ts_slot_count = slots;
     d.fb_cap = c;
   }
+  if (!d.ts_nuniq) HIP_TRY(hipMalloc(&d.ts_nuniq, sizeof(uint32_t)));
+  return 0;
+}
+
+// Batch-leaf launches: clear the verdict bits of equations whose key has an 8-torsion component
+// (dalek verify_batch's randomized domain, answered Err; kernels.hip k_tors_*).  list/count
+// (device) restrict the pass to the comb path's uncached equations; nullptr = all n.  The hash set
+// is sized for the number of candidate equations, which never exceeds n <= fb_cap.
+int launch_torsion(DevCtx& d, const uint8_t* pks, uint64_t* out_words, uint64_t n, const uint32_t* list,
+                   const uint32_t* count, const nwc::Committee& cm, hipStream_t s) {
+  if (n == 0) return 0;
+  if (2 * n > d.ts_slot_count) return set_err(NWC_ERR_ARG, "torsion set too small for %llu equations", (unsigned long long)n);
+  HIP_TRY(hipMemsetAsync(d.ts_slots, 0xFF, 4 * (size_t)d.ts_slot_count, s));
+  HIP_TRY(hipMemsetAsync(d.ts_nuniq, 0, sizeof(uint32_t), s));
+  const nwc::TorsArgs t{pks, out_words, list, count, n, d.ts_slots, d.ts_slot_count - 1, d.ts_uniq, d.ts_nuniq, d.ts_flag, cm};
+  const uint64_t cap = (uint64_t)d.cus * 8;
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, cap);
+  hipLaunchKernelGGL(nwc::k_tors_mark, dim3(grid), dim3(256), 0, s, t);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_tors_eval, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)d.cus * 2)), dim3(256), 0, s, t);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_tors_apply, dim3(grid), dim3(256), 0, s, t);
+  HIP_TRY(hipGetLastError());
   return 0;
 }
 
@@ -323,6 +366,11 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(fgrid), dim3(256), 0, s, a);
     HIP_TRY(hipGetLastError());
   }
+  // batch leaves: keys with torsion (cached keys were checked in the comb kernels; the comb
+  // path's other equations are its uncached list)
+  if (!strict)
+    if (int rc = launch_torsion(d, pks, out_words, n, comb ? d.uc_list : nullptr, comb ? d.uc_count : nullptr, cm, s))
+      return rc;
   HIP_TRY(hipEventRecord(d.scratch_free, s));
   return 0;
 }
@@ -512,6 +560,10 @@ void nwc_shutdown(void) {
     if (d->msg_arena) (void)hipFree(d->msg_arena);
     if (d->uc_list) (void)hipFree(d->uc_list);
     if (d->uc_count) (void)hipFree(d->uc_count);
+    if (d->ts_slots) (void)hipFree(d->ts_slots);
+    if (d->ts_flag) (void)hipFree(d->ts_flag);
+    if (d->ts_uniq) (void)hipFree(d->ts_uniq);
+    if (d->ts_nuniq) (void)hipFree(d->ts_nuniq);
     if (d->scratch_free) (void)hipEventDestroy(d->scratch_free);
     if (d->base_table) (void)hipFree(d->base_table);
     if (d->base16) (void)hipFree(d->base16);

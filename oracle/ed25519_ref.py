@@ -197,30 +197,51 @@ def residual(msg: bytes, pk: bytes, sig: bytes) -> Optional[Point]:
     return pt_add(pt_add(pt_mul(s, BASEPOINT), pt_neg(R)), pt_neg(pt_mul(k, A)))
 
 
-def leaf_ok(msg: bytes, pk: bytes, sig: bytes) -> bool:
-    """A.5 bisection leaf: vote parses, pk and R decode, and e == identity (cofactorless)."""
+def has_torsion(p: Point) -> bool:
+    """A point with a non-zero 8-torsion component: l * P != O (curve25519-dalek 3
+    `EdwardsPoint::is_torsion_free` negated)."""
+    return pt_mul(L, p) != IDENTITY
+
+
+def vote_class(msg: bytes, pk: bytes, sig: bytes) -> str:
+    """One vote of dalek 1.0.1 `verify_batch` (as corrected in round 2).
+
+    dalek checks   -(sum z_i s_i mod l) B + sum z_i R_i + sum (z_i k_i mod l) A_i == O
+    with random 128-bit z_i.  Writing z_i k_i = (z_i k_i mod l) + q_i l, the A-term differs from
+    z_i k_i A_i by q_i (l A_i) = q_i (l T_i), T_i the 8-torsion component of A_i.  So the
+    batch sum is  -sum z_i e_i - sum q_i l T_i  (e_i = s_i B - R_i - k_i A_i), and a vote is
+      "err"         it fails A.1/A.2, or e_i has a prime-order component (Err w.p. 1 - 2^-125);
+      "randomized"  e_i is pure torsion and (e_i != O or T_i != O): the verdict depends on
+                    thread_rng through z_i and q_i = floor(z_i k_i / l);
+      "ok"          e_i == O and A_i is torsion-free (identity included): deterministic Ok.
+    """
     e = residual(msg, pk, sig)
-    return e is not None and e == IDENTITY
+    if e is None:
+        return "err"
+    if pt_mul(8, e) != IDENTITY:
+        return "err"
+    if e != IDENTITY or has_torsion(decompress(pk)):
+        return "randomized"
+    return "ok"
+
+
+def leaf_ok(msg: bytes, pk: bytes, sig: bytes) -> bool:
+    """A.5 bisection leaf = dalek `verify_batch([vote])` decided deterministically: the vote
+    parses, pk and R decode, e == identity (cofactorless) and A is torsion-free.  On the
+    randomized domain the build answers Err (bad vote)."""
+    return vote_class(msg, pk, sig) == "ok"
 
 
 def verify_batch_class(msg: bytes, votes: Sequence[Tuple[bytes, bytes]]) -> str:
     """`crypto::Signature::verify_batch` (crypto/src/lib.rs:206-219) -> dalek `verify_batch` (A.4).
 
-    Returns "ok", "err", or "randomized" (every non-zero residual is pure 8-torsion: the
-    reference's verdict then depends on thread_rng; the build returns Err there).
+    Returns "err" if any vote is "err"; else "randomized" if any vote is (the reference's
+    verdict then depends on thread_rng; the build returns Err there); else "ok".
     """
-    torsion_only = False
-    for pk, sig in votes:
-        e = residual(msg, pk, sig)
-        if e is None:
-            return "err"
-        if e == IDENTITY:
-            continue
-        if pt_mul(8, e) == IDENTITY:
-            torsion_only = True
-        else:
-            return "err"
-    return "randomized" if torsion_only else "ok"
+    classes = [vote_class(msg, pk, sig) for pk, sig in votes]
+    if "err" in classes:
+        return "err"
+    return "randomized" if "randomized" in classes else "ok"
 
 
 def verify_batch(msg: bytes, votes: Sequence[Tuple[bytes, bytes]]) -> bool:
@@ -230,14 +251,23 @@ def verify_batch(msg: bytes, votes: Sequence[Tuple[bytes, bytes]]) -> bool:
 
 def verify_batch_dalek_sampled(msg: bytes, votes: Sequence[Tuple[bytes, bytes]],
                                rng: random.Random) -> bool:
-    """One draw of the reference's randomized equation (random 128-bit z_i), for tests of
-    the randomized domain only."""
-    acc = IDENTITY
+    """One draw of dalek 1.0.1 `verify_batch`'s equation as the crate computes it
+    (crypto/src/lib.rs:218): random 128-bit z_i (thread_rng stands in for the merlin-seeded
+    RNG), the basepoint coefficient -(sum z_i s_i) mod l, z_i on R_i and (z_i k_i mod l) on A_i."""
+    bcoef, acc = 0, IDENTITY
     for pk, sig in votes:
-        e = residual(msg, pk, sig)
-        if e is None:
+        if not sig_scalar_ok(sig):
             return False
-        acc = pt_add(acc, pt_mul(rng.getrandbits(128), e))
+        A = decompress(pk)
+        R = decompress(sig[:32])
+        if A is None or R is None:
+            return False
+        k = scalar_from_hash(sha512(sig[:32] + pk + msg))
+        s = int.from_bytes(sig[32:], "little")
+        z = rng.getrandbits(128)
+        bcoef = (bcoef + z * s) % L
+        acc = pt_add(acc, pt_add(pt_mul(z, R), pt_mul(z * k % L, A)))
+    acc = pt_add(acc, pt_mul((-bcoef) % L, BASEPOINT))
     return acc == IDENTITY
 
 

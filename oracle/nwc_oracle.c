@@ -437,24 +437,19 @@ int orc_verify_strict(const u8 msg32[32], const u8 pk[32], const u8 sig[64]) {
   return ge_eq(Rp, R);
 }
 
-/* A.5 leaf: parses, decodes, and s*B - R - k*A == identity (cofactorless). */
-int orc_leaf(const u8 msg32[32], const u8 pk[32], const u8 sig[64]) {
-  ensure_init();
-  if (!sig_scalar_ok(sig)) return 0;
-  ge A, R;
-  if (!ge_decompress(&A, pk)) return 0;
-  if (!ge_decompress(&R, sig)) return 0;
-  u8 h[64], k[32];
-  sha512_ctx c; sha512_init(&c);
-  sha512_update(&c, sig, 32); sha512_update(&c, pk, 32); sha512_update(&c, msg32, 32);
-  sha512_final(&c, h);
-  sc_reduce512(k, h);
-  ge Rp = ge_double_scalarmult_vartime(k, ge_neg(A), sig + 32);
-  return ge_eq(Rp, R);
-}
+/* l * P != O: P has a non-zero 8-torsion component (curve25519-dalek 3 is_torsion_free, negated) */
+static const u8 L_BYTES[32] = {0xed, 0xd3, 0xf5, 0x5c, 0x1a, 0x63, 0x12, 0x58, 0xd6, 0x9c, 0xf7, 0xa2, 0xde, 0xf9,
+                               0xde, 0x14, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x10};
+static int ge_has_torsion(ge p) { return !ge_is_identity(ge_scalarmult(L_BYTES, p)); }
 
-/* Residual class for the batch domain: 0 = e == O, 1 = pure torsion, 2 = prime part, -1 = parse/decode fail */
-int orc_residual_class(const u8 msg32[32], const u8 pk[32], const u8 sig[64]) {
+/* One vote of dalek 1.0.1 verify_batch (crypto/src/lib.rs:206-219).  dalek checks
+     -(sum z_i s_i mod l) B + sum z_i R_i + sum (z_i k_i mod l) A_i == O
+   with random 128-bit z_i.  With z_i k_i = (z_i k_i mod l) + q_i l the sum is
+   -sum z_i e_i - sum q_i (l A_i), e_i = s_i B - R_i - k_i A_i, and l A_i = l T_i for the 8-torsion
+   component T_i of A_i.  Class: -1 = parse/decode failure, 2 = e_i has a prime-order component
+   (Err w.p. 1 - 2^-125), 1 = randomized (e_i pure torsion, and e_i != O or T_i != O: the verdict
+   depends on z_i and q_i = floor(z_i k_i / l)), 0 = deterministic Ok. */
+int orc_vote_class(const u8 msg32[32], const u8 pk[32], const u8 sig[64]) {
   ensure_init();
   if (!sig_scalar_ok(sig)) return -1;
   ge A, R;
@@ -467,8 +462,15 @@ int orc_residual_class(const u8 msg32[32], const u8 pk[32], const u8 sig[64]) {
   sc_reduce512(k, h);
   ge Rp = ge_double_scalarmult_vartime(k, ge_neg(A), sig + 32);
   ge e = ge_add(Rp, ge_neg(R));
-  if (ge_is_identity(e)) return 0;
-  return ge_is_small_order(e) ? 1 : 2;
+  if (!ge_is_small_order(e)) return 2;
+  if (!ge_is_identity(e) || ge_has_torsion(A)) return 1;
+  return 0;
+}
+
+/* A.5 leaf = dalek verify_batch([vote]) decided deterministically: parses, decodes,
+   s*B - R - k*A == identity (cofactorless) and A torsion-free.  The randomized domain is Err. */
+int orc_leaf(const u8 msg32[32], const u8 pk[32], const u8 sig[64]) {
+  return orc_vote_class(msg32, pk, sig) == 0;
 }
 
 /* crypto::Signature::verify_batch: one digest, n votes (pk_i, sig_i). Deterministic build

@@ -374,6 +374,41 @@ def batch_fixtures(rng, keys, digest):
     add("all-zero-sig-alone", msg, [(votes[0][0], bytes(64))], "R = 00..00 order-4, prime residual")
     add("small-order-A-in-batch", msg, [votes[0], (so_enc := o.compress(so[2]), votes[1][1])],
         "small-order A accepted by batch parse; equation fails")
+    # -- round 2: torsion-bearing A with a zero residual (e = O).  dalek scales A_i by
+    #    (z_i k_i mod l), so l*T_i enters the batch sum with a random multiple: randomized.
+    for j, T in enumerate(so[1:]):
+        Ab = o.compress(o.pt_add(o.pt_mul(a, o.BASEPOINT), T))
+        for trial in range(256):
+            r = o.scalar_from_hash(o.sha512(b"kT0-%d-%d" % (j, trial)))
+            Rb = o.compress(o.pt_mul(r, o.BASEPOINT))
+            k = o.scalar_from_hash(o.sha512(Rb + Ab + msg))
+            if o.pt_mul(k, T) == o.IDENTITY:
+                break
+        else:
+            raise AssertionError("no k with k*T = O")
+        v = (Ab, Rb + le((r + k * a) % o.L))
+        assert o.residual(msg, *v) == o.IDENTITY
+        add("mixed-order-A-T%d-kT0-in-batch" % j, msg, [votes[0], votes[1], v, votes[2]],
+            "A = aB + T, e = O: reference randomized through (z k mod l) A")
+    # small-order A = T with e = O: R = rB + T' where T' = -k T (k depends on R's bytes)
+    for j, T in enumerate(so[1:4]):
+        Ab = o.compress(T)
+        done = None
+        for trial in range(256):
+            r = o.scalar_from_hash(o.sha512(b"soA-%d-%d" % (j, trial)))
+            for Tp in so:
+                Rb = o.compress(o.pt_add(o.pt_mul(r, o.BASEPOINT), Tp))
+                k = o.scalar_from_hash(o.sha512(Rb + Ab + msg))
+                if o.pt_add(Tp, o.pt_mul(k, T)) == o.IDENTITY:
+                    done = (Ab, Rb + le(r))
+                    break
+            if done:
+                break
+        assert done and o.residual(msg, *done) == o.IDENTITY
+        add("small-order-A-T%d-zero-residual" % j, msg, [votes[0], done],
+            "A small-order, e = O: reference randomized (strict rejects it)")
+    # identity A with e = O stays deterministic Ok (l * O = O)
+    add("identity-A-zero-residual", msg, [(ident, ident + le(0)), votes[1]], "A = identity, e = O: Ok")
     return out
 
 
@@ -386,8 +421,8 @@ def main():
     for b in batches:
         if b["class"] == "randomized":
             votes = [(bytes.fromhex(p), bytes.fromhex(s)) for p, s in b["votes"]]
-            draws = [o.verify_batch_dalek_sampled(bytes.fromhex(b["msg"]), votes, random.Random(i)) for i in range(8)]
-            b["reference_draws_ok"] = sum(draws)
+            draws = [o.verify_batch_dalek_sampled(bytes.fromhex(b["msg"]), votes, random.Random(i)) for i in range(16)]
+            b["reference_draws_ok_of_16"] = sum(draws)
     with open(os.path.join(HERE, "sha512.json"), "w") as f:
         json.dump(sha, f, indent=1)
     with open(os.path.join(HERE, "ed25519_verify.json"), "w") as f:

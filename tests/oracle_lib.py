@@ -20,7 +20,7 @@ class Oracle:
         vp, sz = ctypes.c_void_p, ctypes.c_size_t
         lib.orc_verify_strict.argtypes = [vp, vp, vp]
         lib.orc_leaf.argtypes = [vp, vp, vp]
-        lib.orc_residual_class.argtypes = [vp, vp, vp]
+        lib.orc_vote_class.argtypes = [vp, vp, vp]
         lib.orc_verify_batch.argtypes = [vp, vp, vp, sz, vp]
         lib.orc_sha512.argtypes = [vp, sz, vp]
         lib.orc_public_key.argtypes = [vp, vp]

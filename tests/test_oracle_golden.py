@@ -131,3 +131,49 @@ def test_straus_batch_port_matches_leaves(oracle):
     exp, _ = oracle.batch_many(digests, offs, pks, sigs)
     got = oracle.batch_straus_many(digests, offs, pks, sigs)
     assert (got == exp).all() and exp[-1] and not exp[3] and (~exp).sum() >= 3
+
+
+def _golden_batches(golden_verify, golden_batch):
+    """Every golden batch, and every 32-byte-message strict case as a one-vote batch."""
+    out = []
+    for c in golden_verify["cases"]:
+        m = bytes.fromhex(c["msg"])
+        if len(m) == 32:
+            out.append((c["name"], m, [(bytes.fromhex(c["pk"]), bytes.fromhex(c["sig"]))], c["batch1"]))
+    for b in golden_batch:
+        out.append((b["name"], bytes.fromhex(b["msg"]),
+                    [(bytes.fromhex(p), bytes.fromhex(s)) for p, s in b["votes"]], b["class"]))
+    return out
+
+
+def test_c_vote_class_matches_fixtures(oracle, golden_verify, golden_batch):
+    """orc_vote_class (the C restatement of one dalek verify_batch vote) agrees with the Python
+    restatement's class recorded in the fixtures; -1/2 = err, 1 = randomized, 0 = ok."""
+    names = {-1: "err", 2: "err", 1: "randomized", 0: "ok"}
+    for name, m, votes, cls in _golden_batches(golden_verify, golden_batch):
+        got = [names[oracle.lib.orc_vote_class(oracle._p(m), oracle._p(p), oracle._p(s))] for p, s in votes]
+        exp = "err" if "err" in got else ("randomized" if "randomized" in got else "ok")
+        assert exp == cls, name
+
+
+def test_straus_port_over_golden_cases(oracle, golden_verify, golden_batch):
+    """The C port of dalek 1.0.1's verify_batch algorithm (random 128-bit z_i, (z_i hram_i mod l)
+    on A_i, one Straus MSM; oracle/nwc_oracle.c orc_verify_batch_straus) run over 200 seeds on
+    every golden batch and every strict case as a one-vote batch:
+      class "ok"         -> accepted 200/200 (deterministic Ok: the build's Ok)
+      class "err"        -> accepted 0/200
+      class "randomized" -> accepted sometimes, never by a clear majority (the build returns Err)."""
+    D = 200
+    for name, m, votes, cls in _golden_batches(golden_verify, golden_batch):
+        n = len(votes)
+        digests = np.tile(np.frombuffer(m, dtype=np.uint8), (D, 1))
+        offs = (np.arange(D + 1) * n).astype(np.uint32)
+        pks = np.tile(np.frombuffer(b"".join(p for p, _ in votes) or b"\0" * 32, dtype=np.uint8).reshape(-1, 32), (D, 1))
+        sigs = np.tile(np.frombuffer(b"".join(s for _, s in votes) or b"\0" * 64, dtype=np.uint8).reshape(-1, 64), (D, 1))
+        acc = int(oracle.batch_straus_many(digests, offs, pks, sigs).sum())
+        if cls == "ok":
+            assert acc == D, (name, acc)
+        elif cls == "err":
+            assert acc == 0, (name, acc)
+        else:
+            assert 0 < acc <= D // 2 + 30, (name, acc)
