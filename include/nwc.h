@@ -94,6 +94,9 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
 #define NWC_DAG_SERIALIZATION_ERROR 8
 #define NWC_DAG_UNEXPECTED_VOTE 9
 #define NWC_DAG_UNEXPECTED_MESSAGE 10
+/* not a DagError: decoding a PublicKey whose base64 gives < 32 bytes panics in the reference
+ * (crypto/src/lib.rs:75 `bytes[..32]`, inside bincode::deserialize at primary/src/primary.rs:230) */
+#define NWC_DAG_DECODE_PANIC 11
 
 /* Core::sanitize_header / sanitize_vote / sanitize_certificate (primary/src/core.rs:306-346)
  * for a batch of wire messages, each the bincode bytes of a PrimaryMessage as received by

@@ -21,13 +21,19 @@
 //                 Q x 32-B digest, 32-B id, 64-B signature
 //   Vote        = 32-B id, u64 round, str origin, str author, 64-B signature
 //   Certificate = Header, u64 V, V x (str key, 64-B signature)
-//   str         = u64 length, bytes: a PublicKey is the standard base64 of its 32 bytes.
-// Decoding subset: a key string is accepted iff it is the canonical padded standard base64 of 32
-// bytes (44 characters, the 2 trailing bits of the last symbol zero) -- what every honest node
-// sends (base64::encode).  base64 0.13 may accept other forms (unpadded strings, longer strings
-// whose first 32 decoded bytes are used); those are reported as SerializationError here
-// (parity unpinned).  Trailing bytes after a message are ignored, as bincode's
-// legacy config does.
+//   str         = u64 length, bytes.
+// Decoding follows the reference exactly:
+//   * a PublicKey is a serde String decoded by PublicKey::decode_base64 (crypto/src/lib.rs:73-79):
+//     base64 0.13 `decode` (b64_013_check below; padding optional, no trailing bits, '=' only at
+//     the end of the last 8-symbol chunk) and `bytes[..32]`, which PANICS when fewer than 32 bytes
+//     decode -- reported as DAG_DECODE_PANIC; longer decodes use their first 32 bytes.  Key strings
+//     may have any length, so votes have no fixed stride (fast path: every key 44 bytes);
+//   * Header.payload is a BTreeMap<Digest, WorkerId> and Header.parents a BTreeSet<Digest>
+//     (primary/src/messages.rs:17-18): serde inserts the entries one by one, so the decoded header
+//     -- and Header::digest (:75-81) and the worker check (:57-61) -- sees them sorted by digest
+//     bytes, duplicates dropped, a map keeping the LAST value of a key (canon_set / canon_map);
+//   * the first failing field in wire order decides between SerializationError and the panic;
+//     trailing bytes after a message are ignored, as bincode's legacy config does.
 #pragma once
 #include <stdint.h>
 
@@ -45,6 +51,7 @@ enum DagCode : u32 {
   DAG_SERIALIZATION = 8,          // DagError::SerializationError
   DAG_UNEXPECTED_VOTE = 9,        // DagError::UnexpectedVote
   DAG_UNEXPECTED_MESSAGE = 10,    // CertificatesRequest (not a Core message)
+  DAG_DECODE_PANIC = 11,          // the reference panics decoding a key (crypto/src/lib.rs:75 bytes[..32])
 };
 enum MsgKind : u32 { MSG_HEADER = 0, MSG_VOTE = 1, MSG_CERTIFICATE = 2, MSG_OTHER = 3 };
 
@@ -115,36 +122,70 @@ __device__ __forceinline__ i32 b64_val(u32 c) {
   v = (c == '/') ? 63 : v;
   return v;
 }
-// 44 characters (11 words) -> 32 bytes; false unless canonical padded standard base64
-__device__ __forceinline__ bool b64_decode32(const u32 s[11], u32 out[8]) {
+// base64 0.13 `decode` (STANDARD config: standard alphabet, padding not required on decode,
+// decode_allow_trailing_bits = false) of data[pos, pos + L), as PublicKey::decode_base64 runs it
+// (crypto/src/lib.rs:73-79), followed by `bytes[..32]`:
+//   KEY_ERR   a DecodeError: L % 8 in {1, 5}; a byte outside the alphabet ('=' included) in any
+//             8-symbol chunk but the last; in the last chunk a '=' at a position i with i % 4 < 2
+//             or a symbol after a '='; non-zero bits past the last whole output byte;
+//   KEY_PANIC it decodes to fewer than 32 bytes (`bytes[..32]` panics);
+//   KEY_OK    otherwise (the key is the first 32 decoded bytes = symbols 0..42, see b64_first32).
+// Bytes >= 0x80 are never symbols, so the serde String's UTF-8 check cannot change the outcome.
+// Restated in oracle/messages_ref.py b64_013_decode.
+enum KeyStatus : u32 { KEY_OK = 0, KEY_ERR = 1, KEY_PANIC = 2 };
+__device__ u32 b64_013_check(const uint8_t* base, uint64_t pos, uint64_t L) {
+  if ((L & 3) == 1) return KEY_ERR;   // L % 8 in {1, 5}
+  if (L == 0) return KEY_PANIC;       // decodes to nothing
+  const uint64_t nch = (L + 7) >> 3;
   bool ok = true;
-  u32 bits = 0;   // 24-bit group
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) out[i] = 0;
-  _Pragma("unroll") for (int g = 0; g < 11; ++g) {
-    const u32 word = s[g];
-    bits = 0;
-    _Pragma("unroll") for (int k = 0; k < 4; ++k) {
-      const u32 c = (word >> (8 * k)) & 255u;
-      const int pos = 4 * g + k;
-      if (pos == 43) {
-        ok = ok && (c == '=');
-        bits <<= 6;
+#pragma unroll 1
+  for (uint64_t c = 0; c + 1 < nch; ++c) {
+    u32 w[2];
+    ld_words<2>(base, pos + 8 * c, w);
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) ok = ok && b64_val((w[k >> 2] >> (8 * (k & 3))) & 255u) >= 0;
+  }
+  const int tl = (int)(L - 8 * (nch - 1));
+  u32 w[2];
+  ld_words<2>(base, pos + 8 * (nch - 1), w);
+  int k = 0;
+  bool pad = false;
+  uint64_t acc = 0;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    if (i < tl) {
+      const u32 c = (w[i >> 2] >> (8 * (i & 3))) & 255u;
+      if (c == '=') {
+        ok = ok && (i & 3) >= 2;
+        pad = true;
       } else {
         const i32 v = b64_val(c);
-        ok = ok && (v >= 0);
-        bits = (bits << 6) | (u32)(v & 63);
+        ok = ok && !pad && v >= 0;
+        acc = (acc << 6) | (uint64_t)(v & 63);
+        ++k;
       }
     }
-    // group g gives bytes 3g .. 3g+2 (the last group only 2: bytes 30, 31; its low 8 bits are the
-    // 2 trailing bits of symbol 42 plus the padding and must be zero)
+  }
+  // k is 2, 3, 4, 6, 7 or 8 here when ok (the length and padding rules exclude 0, 1 and 5)
+  ok = ok && k >= 2 && k != 5;
+  const int nb = (6 * k) >> 3, extra = 6 * k - 8 * nb;
+  ok = ok && (acc & ((1ull << extra) - 1)) == 0;
+  if (!ok) return KEY_ERR;
+  return 6 * (nch - 1) + (uint64_t)nb < 32 ? KEY_PANIC : KEY_OK;
+}
+// The first 32 decoded bytes = the big-endian bits of symbols 0..42 (a decode of >= 32 bytes has
+// >= 43 symbols, all before any padding): s[] holds characters 0..43 (character 43 is ignored).
+__device__ __forceinline__ void b64_first32(const u32 s[11], u32 out[8]) {
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) out[i] = 0;
+  _Pragma("unroll") for (int g = 0; g < 11; ++g) {
+    u32 bits = 0;
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) {
+      const i32 v = (4 * g + k < 43) ? b64_val((s[g] >> (8 * k)) & 255u) : 0;
+      bits = (bits << 6) | (u32)(v & 63);
+    }
     _Pragma("unroll") for (int b = 0; b < 3; ++b) {
       const int byte = 3 * g + b;
-      const u32 val = (bits >> (16 - 8 * b)) & 255u;
-      if (byte < 32) out[byte >> 2] |= val << (8 * (byte & 3));
+      if (byte < 32) out[byte >> 2] |= ((bits >> (16 - 8 * b)) & 255u) << (8 * (byte & 3));
     }
-    if (g == 10) ok = ok && ((bits & 255u) == 0);
   }
-  return ok;
 }
 
 // SHA-512[..32] of a 16-byte-aligned buffer (little-endian digest words)
@@ -195,6 +236,7 @@ struct MsgReader {
   const uint8_t* base;
   uint64_t pos, end;
   bool ok;
+  bool panic;   // decoding stopped at a key whose base64 gives < 32 bytes (reference: panic)
   __device__ __forceinline__ bool need(uint64_t n) {
     ok = ok && pos <= end && n <= end - pos;
     return ok;
@@ -215,15 +257,21 @@ struct MsgReader {
     ld_words<16>(base, pos, out);
     pos += 64;
   }
-  // a PublicKey: u64 length 44 + canonical base64
+  // a PublicKey: serde String (u64 length, bytes) + PublicKey::decode_base64
   __device__ __forceinline__ void key(u32 out[8]) {
+    for (int i = 0; i < 8; ++i) out[i] = 0;
     const uint64_t len = u64();
-    ok = ok && len == 44;
-    if (!need(44)) { for (int i = 0; i < 8; ++i) out[i] = 0; return; }
-    u32 s[11];
-    ld_words<11>(base, pos, s);
-    pos += 44;
-    ok = b64_decode32(s, out) && ok;
+    if (!need(len)) return;
+    const u32 st = b64_013_check(base, pos, len);
+    if (st == KEY_OK) {
+      u32 s[11];
+      ld_words<11>(base, pos, s);   // < 44 bytes of string: the rest is padding / the next field
+      b64_first32(s, out);
+    } else {
+      panic = st == KEY_PANIC;      // ok was true: this is the first failure
+      ok = false;
+    }
+    pos += len;
   }
 };
 
@@ -239,11 +287,12 @@ __device__ __forceinline__ uint64_t member_stake(const CommitteeCfg& cc, int idx
 // committees of up to this many authorities (the AuthorityReuse scan keeps one LDS slot each)
 constexpr uint32_t MSG_MAX_COMMITTEE = 4096;
 enum MsgFlag : u32 {
-  MF_PARSE_ERR = 1u << 8,    // bincode / base64 decoding failed
+  MF_PARSE_ERR = 1u << 8,    // bincode / base64 decoding failed (or panicked, MF_PANIC)
   MF_GENESIS = 1u << 9,      // Certificate::genesis(committee).contains(self)
   MF_TOO_OLD = 1u << 10,     // gc_round > round (header, certificate)
   MF_STAKE0 = 1u << 11,      // the author has no voting rights
   MF_WORKER_BAD = 1u << 12,  // a payload worker id the author does not run
+  MF_PANIC = 1u << 13,       // decoding reached a key of < 32 bytes before any error (panic)
 };
 
 __device__ __forceinline__ u32 wave_min_u32(u32 v) {
@@ -257,6 +306,92 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   }
   return v;
 }
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  const u32 lo = (u32)__shfl((int)(u32)v, src, 64), hi = (u32)__shfl((int)(u32)(v >> 32), src, 64);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// ---- BTreeMap / BTreeSet from their bincode sequences (one wave) ----------------------------
+// Digests order as byte strings (Digest derives Ord on [u8; 32]); the words are little-endian.
+__device__ __forceinline__ int dig_cmp(const u32 a[8], const u32 b[8]) {
+  int r = 0;
+  _Pragma("unroll") for (int w = 7; w >= 0; --w) {
+    const u32 x = __builtin_bswap32(a[w]), y = __builtin_bswap32(b[w]);
+    r = x != y ? (x < y ? -1 : 1) : r;
+  }
+  return r;
+}
+// Writes the canonical form of `cnt` wire entries of WORDS words (digest first) at byte offset
+// `src` into the word-aligned `dst` and returns the number of distinct digests:
+//   SET (parents, 8 words): ascending digests, duplicates dropped (BTreeSet::insert keeps one);
+//   MAP (payload, 9 words): ascending digests, one entry per digest with the LAST wire value
+//        (serde's BTreeMap visitor inserts each entry; insert replaces an existing key's value).
+// Strictly ascending input -- what serialising a BTree* produces -- is copied as is.  Otherwise
+// entry e goes to its stable-sort rank (#smaller digests + #equal digests before it; cnt compares
+// per entry) and the sorted run is compacted in place 64 entries per step, keeping the first
+// (SET) or the last (MAP) of each run of equal digests.  Every lane of the wave must call this.
+template <int WORDS, bool MAP>
+__device__ uint64_t canon_entries(const uint8_t* base, uint64_t src, uint64_t cnt, u32* dst, u32 lane) {
+  constexpr uint64_t REC = 4 * WORDS;
+  bool asc = true;
+  for (uint64_t e = lane; e + 1 < cnt; e += 64) {
+    u32 x[8], y[8];
+    ld_words<8>(base, src + REC * e, x);
+    ld_words<8>(base, src + REC * (e + 1), y);
+    asc = asc && dig_cmp(x, y) < 0;
+  }
+  if (__all(asc)) {
+    for (uint64_t k = lane; k < WORDS * cnt; k += 64) dst[k] = ld_u32(base, src + 4 * k);
+    __syncthreads();
+    return cnt;
+  }
+  for (uint64_t e = lane; e < cnt; e += 64) {
+    u32 x[WORDS];
+    ld_words<WORDS>(base, src + REC * e, x);
+    uint64_t pos = 0;
+#pragma unroll 1
+    for (uint64_t j = 0; j < cnt; ++j) {
+      u32 y[8];
+      ld_words<8>(base, src + REC * j, y);
+      const int c = dig_cmp(y, x);
+      pos += (c < 0 || (c == 0 && j < e)) ? 1u : 0u;
+    }
+    _Pragma("unroll") for (int k = 0; k < WORDS; ++k) dst[WORDS * pos + k] = x[k];
+  }
+  __syncthreads();
+  // Compaction: step s reads entries [64 s, 64 s + 64] and writes only below 64 s + 64, so no
+  // step reads what an earlier step wrote; within a step every store depends on every load.
+  uint64_t kept = 0;
+  u32 carry[8];
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) carry[k] = 0;
+  for (uint64_t t0 = 0; t0 < cnt; t0 += 64) {
+    const uint64_t t = t0 + lane;
+    const bool act = t < cnt;
+    u32 x[WORDS];
+    _Pragma("unroll") for (int k = 0; k < WORDS; ++k) x[k] = act ? dst[WORDS * t + k] : 0u;
+    bool keep;
+    if constexpr (MAP) {
+      const bool last = t + 1 >= cnt;
+      u32 y[8];
+      _Pragma("unroll") for (int k = 0; k < 8; ++k) y[k] = (act && !last) ? dst[WORDS * (t + 1) + k] : 0u;
+      keep = act && (last || dig_cmp(x, y) != 0);
+    } else {
+      u32 prev[8];
+      _Pragma("unroll") for (int k = 0; k < 8; ++k) {
+        prev[k] = (u32)__shfl_up((int)x[k], 1, 64);
+        if (lane == 0) prev[k] = carry[k];
+        carry[k] = (u32)__shfl((int)x[k], 63, 64);
+      }
+      keep = act && (t == 0 || dig_cmp(prev, x) != 0);
+    }
+    const uint64_t bal = __ballot(keep);
+    const uint64_t at = kept + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
+    if (keep) _Pragma("unroll") for (int k = 0; k < WORDS; ++k) dst[WORDS * at + k] = x[k];
+    kept += (uint64_t)__popcll(bal);
+  }
+  __syncthreads();
+  return kept;
+}
 
 // One wave (64-thread block) per message.  Every lane runs the sequential field decoding (same
 // instructions, no divergence); vote-, payload- and digest-input loops are split across lanes.
@@ -265,7 +400,7 @@ __global__ __launch_bounds__(64) void k_parse_messages(MsgArgs a, Committee cm, 
   const uint64_t i = blockIdx.x;
   const u32 lane = threadIdx.x;
   if (i >= a.m) return;   // block-uniform
-  MsgReader r{a.data, a.offsets[i], a.offsets[i + 1], true};
+  MsgReader r{a.data, a.offsets[i], a.offsets[i + 1], true, false};
   const uint64_t variant = ld_u32(a.data, r.pos);
   r.need(4);
   r.pos += 4;
@@ -290,56 +425,93 @@ __global__ __launch_bounds__(64) void k_parse_messages(MsgArgs a, Committee cm, 
     r.bytes64(sig);
     const int aidx = r.ok ? committee_lookup(cm, author) : -1;
     const uint64_t astake = member_stake(cc, aidx);
+    // per-message scratch (>= message length + 1 bytes, 128-B aligned): the Header::digest input
+    // (author || round || BTreeMap payload || BTreeSet parents), then the vote offsets
+    u32* d = reinterpret_cast<u32*>(a.hashbuf + ((a.offsets[i] + 127) & ~(uint64_t)127) + 128 * i);
     if (r.ok) {
-      // Committee::worker(author, id) for every payload entry (only consulted for members)
+      if (lane == 0) {
+        _Pragma("unroll") for (int k = 0; k < 8; ++k) d[k] = author[k];
+        d[8] = (u32)round;
+        d[9] = (u32)(round >> 32);
+      }
+      const uint64_t Pc = canon_entries<9, true>(r.base, pay_off, P, d + 10, lane);
+      const uint64_t Qc = canon_entries<8, false>(r.base, par_off, Q, d + 10 + 9 * Pc, lane);
+      // Committee::worker(author, id) for every value of the map (only consulted for members)
       bool wbad = false;
       if (aidx >= 0) {
         const uint32_t w0 = cc.worker_off[aidx], w1 = cc.worker_off[aidx + 1];
-        for (uint64_t e = lane; e < P; e += 64) {
-          const u32 wid = ld_u32(r.base, pay_off + 36 * e + 32);
+        for (uint64_t e = lane; e < Pc; e += 64) {
+          const u32 wid = d[10 + 9 * e + 8];
           bool found = false;
           for (uint32_t k = w0; k < w1; ++k) found = found || (cc.worker_ids[k] == wid);
           wbad = wbad || !found;
         }
       }
       if (__any(wbad)) flags |= MF_WORKER_BAD;
-      // Header::digest input gathered into the 128-B aligned scratch (word-aligned destinations)
-      uint8_t* hb = a.hashbuf + ((a.offsets[i] + 127) & ~(uint64_t)127) + 128 * i;
-      u32* d = reinterpret_cast<u32*>(hb);
-      if (lane == 0) {
-        _Pragma("unroll") for (int k = 0; k < 8; ++k) d[k] = author[k];
-        d[8] = (u32)round;
-        d[9] = (u32)(round >> 32);
-      }
-      const uint64_t pw = P * 9, qw = Q * 8;
-      for (uint64_t k = lane; k < pw; k += 64) d[10 + k] = ld_u32(r.base, pay_off + 4 * k);
-      for (uint64_t k = lane; k < qw; k += 64) d[10 + pw + k] = ld_u32(r.base, par_off + 4 * k);
-      hlen = (u32)(40 + 36 * P + 32 * Q);
+      hlen = (u32)(40 + 36 * Pc + 32 * Qc);
     }
     if (kind == MSG_CERTIFICATE) {
       const uint64_t V = r.u64();
-      r.need(V <= (1ull << 32) ? V * 116 : ~0ull);   // every vote is 116 B (44-character keys)
       const uint64_t votes_off = r.pos;
-      if (r.ok) {
+      digest72(id, round, author, cd);
+      // Vote positions.  Fast path: every key string is 44 bytes (base64::encode of 32 bytes), so
+      // vote v sits at votes_off + 116 v -- true iff each of those length fields reads 44.
+      bool fast = r.ok && V <= (r.end - r.pos) / 116;
+      if (fast) {
+        bool f = true;
+        for (uint64_t v = lane; v < V; v += 64) f = f && ld_u64(r.base, votes_off + 116 * v) == 44;
+        fast = __all(f);
+      }
+      // Otherwise lane 0 walks the list: voff[v] = offset of vote v for the nfull votes wholly
+      // inside the message; `tail` = 1 when the next vote's key string is inside but its signature
+      // is cut (its key still decides panic vs error), 2 when its length or key is cut.
+      u32* voff = d + 12 + 9 * P + 8 * Q;   // past the digest input (P, Q >= the kept counts)
+      uint64_t nfull = V;
+      u32 tail = 0;
+      if (r.ok && !fast) {
+        uint64_t nf = 0;
+        u32 tk = 0;
+        if (lane == 0) {
+          uint64_t cur = votes_off;
+          for (; nf < V; ++nf) {   // every vote takes >= 72 bytes: ends within the message
+            if (r.end - cur < 8) { tk = 2; break; }
+            const uint64_t L = ld_u64(r.base, cur);
+            if (L > r.end - cur - 8) { tk = 2; break; }
+            voff[nf] = (u32)(cur - votes_off);
+            if (r.end - cur - 8 - L < 64) { tk = 1; break; }
+            cur += 8 + L + 64;
+          }
+        }
+        nfull = shfl_u64(nf, 0);
+        tail = (u32)__shfl((int)tk, 0, 64);
+        __syncthreads();   // voff written by lane 0
+      }
+      const bool whole = r.ok && nfull == V;
+      if (whole) {
         u32 vb = 0;
         if (lane == 0) vb = atomicAdd(a.v_total, (uint32_t)V);
         vbase = (u32)__shfl((int)vb, 0, 64);
-        if ((uint64_t)vbase + V > a.v_cap) r.ok = false;
+        if ((uint64_t)vbase + V > a.v_cap) r.ok = false;   // cannot happen: v_cap >= bytes / 72
       }
-      digest72(id, round, author, cd);
       if (r.ok) {
         const uint32_t ncm = cc.n < MSG_MAX_COMMITTEE ? cc.n : MSG_MAX_COMMITTEE;
         for (uint32_t k = lane; k < ncm; k += 64) first[k] = 0xFFFFFFFFu;
         __syncthreads();
-        // pass 1: decode every vote (one per lane), emit its equation, note first positions
-        bool vok = true;
+        // pass 1: decode every vote (one per lane).  The first failing vote in wire order decides
+        // the message (bincode stops there); a whole list also emits its equations and notes
+        // each member's first position.
+        const uint64_t ndec = nfull + (tail == 1 ? 1 : 0);
+        u32 fpos = 0xFFFFFFFFu, fkind = KEY_OK;
         uint64_t weight = 0;
-        for (uint64_t v = lane; v < V; v += 64) {
-          MsgReader vr{a.data, votes_off + 116 * v, votes_off + 116 * v + 116, true};
+        for (uint64_t v = lane; v < ndec; v += 64) {
+          const uint64_t off = votes_off + (fast ? 116 * v : (uint64_t)voff[v]);
+          MsgReader vr{a.data, off, r.end, true, false};
           u32 key[8], sg[16];
           vr.key(key);
+          const u32 st = vr.ok ? (v < nfull ? KEY_OK : KEY_ERR) : (vr.panic ? KEY_PANIC : KEY_ERR);
+          if (st != KEY_OK && (u32)v < fpos) { fpos = (u32)v; fkind = st; }
+          if (!whole) continue;
           vr.bytes64(sg);
-          vok = vok && vr.ok;
           st_words(a.v_pk + 32 * (vbase + v), key, 8);
           st_words(a.v_sig + 64 * (vbase + v), sg, 16);
           a.v_msg[vbase + v] = (uint32_t)i;
@@ -347,34 +519,44 @@ __global__ __launch_bounds__(64) void k_parse_messages(MsgArgs a, Committee cm, 
           weight += member_stake(cc, kidx);
           if (kidx >= 0 && kidx < (int)MSG_MAX_COMMITTEE) atomicMin(&first[kidx], (u32)(v < 0xFFFFFFF0u ? v : 0xFFFFFFF0u));
         }
-        r.ok = __all(vok);
-        __syncthreads();
-        // pass 2: Certificate::verify's vote loop (messages.rs:198-208) stops at the first vote whose
-        // name is already used (AuthorityReuse) or has no stake (UnknownAuthority); while no
-        // error has occurred every earlier vote was inserted, so "used" = all earlier names.
-        u32 err = 0xFFFFFFFFu;
-        u32 err_kind = 0;
-        for (uint64_t v = lane; v < V; v += 64) {
-          const u32* kw = reinterpret_cast<const u32*>(a.v_pk + 32 * (vbase + v));
-          u32 key[8];
-          _Pragma("unroll") for (int k = 0; k < 8; ++k) key[k] = kw[k];
-          const int kidx = committee_lookup(cm, key);
-          const bool reused = kidx >= 0 && kidx < (int)MSG_MAX_COMMITTEE && first[kidx] < (u32)v;
-          const bool unknown = member_stake(cc, kidx) == 0;
-          if ((reused || unknown) && (u32)v < err) { err = (u32)v; err_kind = reused ? DAG_AUTHORITY_REUSE : DAG_UNKNOWN_AUTHORITY; }
+        const u32 fmin = wave_min_u32(fpos);
+        if (fmin != 0xFFFFFFFFu) {
+          const uint64_t owner = __ballot(fpos == fmin);
+          const u32 fk = (u32)__shfl((int)fkind, __ffsll((unsigned long long)owner) - 1, 64);
+          r.ok = false;
+          r.panic = fk == KEY_PANIC;
+        } else if (!whole) {
+          r.ok = false;   // the list is cut inside a vote after every key decoded
         }
-        const u32 emin = wave_min_u32(err);
-        const bool mine = err == emin && emin != 0xFFFFFFFFu;
-        const uint64_t owner = __ballot(mine);
-        const u32 ek = (u32)__shfl((int)err_kind, owner ? __ffsll((unsigned long long)owner) - 1 : 0, 64);
-        const uint64_t wsum = wave_sum_u64(weight);
-        post = emin != 0xFFFFFFFFu ? ek : (wsum < cc.quorum ? DAG_REQUIRES_QUORUM : DAG_OK);
-        vcount = (u32)V;
+        __syncthreads();
+        if (r.ok) {
+          // pass 2: Certificate::verify's vote loop (messages.rs:198-208) stops at the first vote
+          // whose name is already used (AuthorityReuse) or has no stake (UnknownAuthority); while
+          // no error has occurred every earlier vote was inserted, so "used" = all earlier names.
+          u32 err = 0xFFFFFFFFu;
+          u32 err_kind = 0;
+          for (uint64_t v = lane; v < V; v += 64) {
+            const u32* kw = reinterpret_cast<const u32*>(a.v_pk + 32 * (vbase + v));
+            u32 key[8];
+            _Pragma("unroll") for (int k = 0; k < 8; ++k) key[k] = kw[k];
+            const int kidx = committee_lookup(cm, key);
+            const bool reused = kidx >= 0 && kidx < (int)MSG_MAX_COMMITTEE && first[kidx] < (u32)v;
+            const bool unknown = member_stake(cc, kidx) == 0;
+            if ((reused || unknown) && (u32)v < err) { err = (u32)v; err_kind = reused ? DAG_AUTHORITY_REUSE : DAG_UNKNOWN_AUTHORITY; }
+          }
+          const u32 emin = wave_min_u32(err);
+          const bool mine = err == emin && emin != 0xFFFFFFFFu;
+          const uint64_t owner = __ballot(mine);
+          const u32 ek = (u32)__shfl((int)err_kind, owner ? __ffsll((unsigned long long)owner) - 1 : 0, 64);
+          const uint64_t wsum = wave_sum_u64(weight);
+          post = emin != 0xFFFFFFFFu ? ek : (wsum < cc.quorum ? DAG_REQUIRES_QUORUM : DAG_OK);
+          vcount = (u32)V;
+        }
       }
     }
     if (!r.ok) {
-      flags |= MF_PARSE_ERR;
-      vcount = 0;   // (slots of a failed vote list keep the host's zero-filled v_msg: index 0 is valid)
+      flags |= MF_PARSE_ERR | (r.panic ? MF_PANIC : 0u);
+      vcount = 0;   // (slots of a failed vote list keep v_msg = i or the host's zero fill: valid indices)
     } else {
       u32 z = 0;
       _Pragma("unroll") for (int k = 0; k < 8; ++k) z |= id[k];
@@ -393,7 +575,7 @@ __global__ __launch_bounds__(64) void k_parse_messages(MsgArgs a, Committee cm, 
     r.bytes64(sg);
     digest72(id, round, origin, dig);
     if (!r.ok) {
-      flags |= MF_PARSE_ERR;
+      flags |= MF_PARSE_ERR | (r.panic ? MF_PANIC : 0u);
     } else if (a.target.enabled && a.target.round > round) {
       post = DAG_TOO_OLD;   // Core::sanitize_vote (primary/src/core.rs:319-322)
     } else if (a.target.enabled && !(words_eq8(id, a.target.id) && words_eq8(origin, a.target.origin) &&
@@ -461,7 +643,7 @@ __global__ void k_finalize_messages(const uint32_t* __restrict__ rec, const uint
   if (kind == MSG_OTHER) {
     code = post;
   } else if (r0 & MF_PARSE_ERR) {
-    code = DAG_SERIALIZATION;
+    code = (r0 & MF_PANIC) ? DAG_DECODE_PANIC : DAG_SERIALIZATION;
   } else if (kind == MSG_VOTE) {
     code = post != DAG_OK ? post : (sig_ok ? DAG_OK : DAG_INVALID_SIGNATURE);
   } else if (r0 & MF_TOO_OLD) {

@@ -916,7 +916,7 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
 // Sizes the arena from `total`; one D2H sync reads the number of vote equations.
 static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total, uint64_t gc_round,
                  const uint8_t* vote_target, int32_t* dcodes, uint8_t* ddigests, uint32_t* drec, hipStream_t s) {
-  const uint64_t vcap = total / 116 + 1;
+  const uint64_t vcap = total / 72 + 1;   // a vote list is allocated only when wholly inside its message (>= 72 B per vote)
   const size_t need = align256(total + 128 * (m + 2)) + align256(32 * m) * 3 + align256(64 * m) +
                       align256(32 * vcap) + align256(64 * vcap) + align256(4 * vcap) + align256(4) +
                       align256(4 * m) + align256(16 * m) + align256(4 * m) +

@@ -29,7 +29,7 @@ __all__ = ["DagError", "Authority", "Committee", "Header", "Vote", "Certificate"
 
 DAG_ERRORS = ["Ok", "InvalidSignature", "InvalidHeaderId", "MalformedHeader", "UnknownAuthority",
               "AuthorityReuse", "CertificateRequiresQuorum", "TooOld", "SerializationError", "UnexpectedVote",
-              "UnexpectedMessage"]
+              "UnexpectedMessage", "DecodePanic"]
 
 
 class DagError(Exception):

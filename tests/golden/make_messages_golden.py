@@ -168,6 +168,92 @@ def main():
     huge[off:off + 8] = struct.pack("<Q", 1 << 40)
     add("cert-huge-vote-count", bytes(huge), RES)
 
+    # ---- round 2: BTreeMap / BTreeSet canonicalisation (primary/src/messages.rs:17-18, 75-81) ------
+    CAN = "restatement: serde builds the BTreeMap/BTreeSet (sorted, deduplicated, last value wins)"
+
+    def wire_header(k, parents, payload, id_over_wire=False, round_=2):
+        """Header of key k sent with entries in the given (wire) order; its id is Header::digest of
+        the canonical form, or (id_over_wire) of the wire order as a confused peer might compute."""
+        if id_over_wire:
+            b = pks[k] + struct.pack("<Q", round_)
+            for d, w in payload:
+                b += d + struct.pack("<I", w)
+            hid = mr.sha512_32(b + b"".join(parents))
+        else:
+            hid = mr.header_id(pks[k], round_, payload, parents)
+        return mr.enc_header(pks[k], round_, payload, parents, hid, ed.sign(seeds[k], hid), wire_order=True), hid
+
+    P = [bytes([v] * 32) for v in (200, 13, 150, 7, 99, 42)]              # distinct digests, not sorted
+    assert sorted(P) != P
+    for name, parents, payload, over_wire in [
+            ("header-unsorted-parents", P, [], False),
+            ("header-duplicate-parents", P[:3] + P[:2] + P[3:], [], False),
+            ("header-unsorted-parents-id-over-wire-order", P, [], True),
+            ("header-duplicate-parents-id-over-wire-order", P[:3] + [P[0]] + P[3:], [], True),
+            ("header-unsorted-payload", [], [(P[4], 0), (P[1], 0), (P[2], 0)], False),
+            ("header-duplicate-payload-bad-then-good", P[:2], [(P[3], 1), (P[1], 0), (P[3], 0)], False),
+            ("header-duplicate-payload-good-then-bad", P[:2], [(P[3], 0), (P[1], 0), (P[3], 1)], False),
+            ("header-duplicate-payload-same", P[:2], [(P[3], 0), (P[3], 0), (P[0], 0)], False),
+            ("header-many-unsorted", [bytes([(i * 101 + 7) % 256] * 32) for i in range(150)] +
+             [bytes([(i * 101 + 7) % 256] * 32) for i in range(0, 150, 7)],
+             [(bytes([(i * 53 + 1) % 256] * 32), 0) for i in range(70)] + [(bytes([54] * 32), 0)], False)]:
+        hb, hid = wire_header(1, parents, payload, over_wire)
+        add(name, mr.msg_header(hb), CAN)
+        # the same header inside a certificate with the committee's votes on it
+        vs = [(pks[j], ed.sign(seeds[j], mr.digest72(hid, 2, pks[1]))) for j in range(4)]
+        add(name.replace("header-", "cert-", 1), C(hb, vs), CAN)
+
+    # ---- round 2: base64 0.13 key forms (crypto/src/lib.rs:73-79) ---------------------------------
+    B64R = "restatement of base64 0.13 decode + bytes[..32] (crypto/src/lib.rs:73-79)"
+    import base64 as _b64
+
+    def forms_of(pk):
+        k = _b64.b64encode(pk)
+        return {
+            "unpadded-43": k[:43],
+            "long-88": _b64.b64encode(pk + bytes(range(32))),            # first 32 bytes are the key
+            "long-45-unpadded": _b64.b64encode(pk + b"\x07\x09").rstrip(b"="),
+            "long-48": _b64.b64encode(pk + b"\x01\x02\x03\x04"),
+            "short-31-bytes": _b64.b64encode(pk[:31]),                   # decodes to 31 bytes: panic
+            "empty": b"",                                                # 0 bytes: panic
+            "short-40-chars": k[:40],                                    # 30 bytes: panic
+            "pad-at-42": k[:42] + b"==",                                 # '=' at chunk position 2, too early
+            "len-45": k + b"A",                                          # 45 % 8 == 5: InvalidLength
+            "len-41": k[:41],                                            # 41 % 8 == 1
+            "pad-then-symbol": k[:43] + b"=A==",
+            "non-utf8": k[:20] + b"\xff" + k[21:],
+            "space": k[:43] + b" ",
+            "nonzero-trailing-unpadded": k[:42] + mr.B64[mr.B64.index(chr(k[42])) | 1].encode(),
+        }
+
+    f1 = forms_of(pks[1])
+    for fname, text in f1.items():
+        hid = mr.header_id(pks[1], 3, [], [])
+        hb = mr.enc_header(pks[1], 3, [], [], hid, ed.sign(seeds[1], hid), author_text=text)
+        add("b64-header-author-" + fname, mr.msg_header(hb), B64R)
+        add("b64-cert-vote1-" + fname, C(hdr_bytes(h3), votes3, key_texts=[None, text, None, None]), B64R)
+        add("b64-vote-author-" + fname,
+            struct.pack("<I", 1) + h3[4] + struct.pack("<Q", 1) + mr.enc_key(h3[0]) + mr.enc_key(pks[1], text) +
+            vote_sig(h3, 1), B64R, target=target)
+    add("b64-vote-origin-unpadded", struct.pack("<I", 1) + h3[4] + struct.pack("<Q", 1) +
+        mr.enc_key(h3[0], forms_of(h3[0])["unpadded-43"]) + mr.enc_key(pks[1]) + vote_sig(h3, 1), B64R, target=target)
+    # the first failing vote decides: a panicking key before an invalid one, and after it
+    f2 = forms_of(pks[2])
+    add("b64-cert-panic-then-error", C(hdr_bytes(h3), votes3, key_texts=[None, f1["empty"], f2["len-45"], None]), B64R)
+    add("b64-cert-error-then-panic", C(hdr_bytes(h3), votes3, key_texts=[None, f1["len-45"], f2["empty"], None]), B64R)
+    full = C(hdr_bytes(h3), votes3, key_texts=[None, None, None, forms_of(pks[3])["short-31-bytes"]])
+    add("b64-cert-panic-in-truncated-last-vote", full[:-10], B64R)
+    add("b64-cert-truncated-in-key-of-panic-vote", full[:-64 - 3], B64R)
+    mixed = [None, f1["unpadded-43"], f2["long-88"], forms_of(pks[3])["long-48"]]
+    add("b64-cert-mixed-key-lengths", C(hdr_bytes(h3), votes3, key_texts=mixed), B64R)
+    add("b64-cert-mixed-key-lengths-reuse", C(hdr_bytes(h3), votes3 + [votes3[1]], key_texts=mixed + [f1["long-48"]]),
+        B64R)
+    add("b64-cert-mixed-key-lengths-bad-sig", C(hdr_bytes(h3), badv, key_texts=mixed), B64R)
+    add("b64-cert-mixed-key-lengths-unsorted-header",
+        C(wire_header(1, P, [], False, round_=2)[0],
+          [(pks[j], ed.sign(seeds[j], mr.digest72(wire_header(1, P, [], False, round_=2)[1], 2, pks[1])))
+           for j in range(4)], key_texts=[f1 and forms_of(pks[0])["long-88"], f1["unpadded-43"], None, None]), B64R)
+
     out = {"committee": {"keys": [p.hex() for p in pks], "stakes": [1] * 4, "workers": [[0]] * 4,
                          "source": "primary/src/tests/common.rs committee()"},
            "outsider": outsider.hex(), "cases": cases}

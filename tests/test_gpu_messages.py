@@ -101,8 +101,29 @@ def _random_batch(oracle, rng, N=100, ncert=300, nhdr=100, nvote=200):
         payload = [(bytes(rng.integers(0, 256, 32, dtype=np.uint8)), int(rng.integers(0, 2)))
                    for _ in range(int(rng.integers(0, 3)))]
         payload = [(d, w if w in workers[k % N] or rng.random() < 0.3 else 0) for d, w in payload]
+        if rng.random() < 0.15 and parents:      # Byzantine wire order: duplicates, unsorted
+            parents = parents + [parents[int(rng.integers(0, len(parents)))]]
+        if rng.random() < 0.15 and payload:
+            d0, _ = payload[int(rng.integers(0, len(payload)))]
+            payload = payload + [(d0, int(rng.integers(0, 2)))]
+        if rng.random() < 0.1:
+            parents.reverse()
+            payload.reverse()
         hid = mr.header_id(pks[k], rnd, payload, parents)
         return [pks[k], rnd, payload, parents, hid, oracle.sign(seeds[k], hid)]
+
+    import base64
+
+    def key_text(pk, p=0.1):
+        """base64 0.13 accepts more than base64::encode emits (crypto/src/lib.rs:73-79)."""
+        if rng.random() >= p:
+            return None
+        u = 0.9 + 0.1 * rng.random()
+        if u < 0.94:
+            return base64.b64encode(pk)[:43]                        # unpadded
+        if u < 0.97:
+            return base64.b64encode(pk + bytes(int(rng.integers(1, 40))))   # longer decode
+        return base64.b64encode(pk[:int(rng.integers(0, 32))])       # < 32 bytes: panic
 
     msgs = []
     for _ in range(ncert):
@@ -132,7 +153,8 @@ def _random_batch(oracle, rng, N=100, ncert=300, nhdr=100, nvote=200):
             j = int(rng.integers(0, len(votes)))
             s = votes[j][1]
             votes[j] = (votes[j][0], s[:45] + bytes([s[45] ^ 8]) + s[46:])
-        m = mr.msg_certificate(mr.enc_header(*h), votes)
+        m = mr.msg_certificate(mr.enc_header(*h, wire_order=True, author_text=key_text(h[0])), votes,
+                               key_texts=[key_text(kk, 0.005) for kk, _ in votes])
         if rng.random() < 0.02:
             m = m[:int(rng.integers(0, len(m)))]
         msgs.append(m)
@@ -141,7 +163,7 @@ def _random_batch(oracle, rng, N=100, ncert=300, nhdr=100, nvote=200):
         h = header(k, int(rng.integers(0, 50)))
         if rng.random() < 0.05:
             h[5] = bytes(64)
-        msgs.append(mr.msg_header(mr.enc_header(*h)))
+        msgs.append(mr.msg_header(mr.enc_header(*h, wire_order=True, author_text=key_text(h[0]))))
     for _ in range(nvote):
         k = int(rng.integers(0, N + 5 if rng.random() < 0.05 else N))
         hid = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
@@ -150,7 +172,8 @@ def _random_batch(oracle, rng, N=100, ncert=300, nhdr=100, nvote=200):
         s = oracle.sign(seeds[k], mr.digest72(hid, rnd, origin))
         if rng.random() < 0.05:
             s = s[:10] + bytes([s[10] ^ 1]) + s[11:]
-        msgs.append(mr.msg_vote(hid, rnd, origin, pks[k], s))
+        msgs.append(struct.pack("<I", 1) + hid + struct.pack("<Q", rnd) + mr.enc_key(origin, key_text(origin)) +
+                    mr.enc_key(pks[k], key_text(pks[k])) + s)
     order = rng.permutation(len(msgs))
     return committee, pks[:N], stakes, workers, [msgs[i] for i in order]
 
@@ -169,8 +192,8 @@ def test_random_batches_vs_oracle(lib, oracle):
                 assert codes[i] == code, (i, int(codes[i]), mr.NAMES[code])
                 if kind in (0, 1, 2):
                     assert dig[i].tobytes() == d, i
-        counts = np.bincount(codes, minlength=11)
-        assert counts[0] > 100 and counts[1] > 5 and counts[6] > 3   # the mix exercises the paths
+        counts = np.bincount(codes, minlength=12)
+        assert counts[0] > 100 and counts[1] > 5 and counts[6] > 3 and counts[11] > 3   # the mix exercises the paths
     finally:
         lib.nwc_set_committee(None, 0)
 
