@@ -149,6 +149,16 @@ int nwc_dev_keygen_sign(const void* d_seeds, const void* d_msgs, uint64_t n, voi
 /* Select the HIP device used by nwc_dev_* on the calling thread (index into the init mask). */
 int nwc_dev_set_device(int device);
 
+/* ---- sharding (host only; no device needed) --------------------------------------------- */
+/* independent units split over `world` GPUs/ranks.  [*lo, *hi) of n units for
+ * `rank`: contiguous, every shard but the last starts on a multiple of 64 (whole verdict words),
+ * so shards never share a byte of a verdict bitmap.  Used by the host entry points' per-device
+ * threads and mirrored by narwhal_amd/shard.py shard_bounds for one-process-per-GPU runs. */
+int nwc_shard_bounds(uint64_t n, uint32_t world, uint32_t rank, uint64_t* lo, uint64_t* hi);
+/* Vote-index cuts (world + 1 values, cuts[0] = 0, cuts[world] = offsets[m]) on certificate
+ * boundaries, balanced by vote count: a certificate's votes never split (config 3). */
+int nwc_cert_cuts(const uint32_t* offsets, size_t m, uint32_t world, uint64_t* cuts);
+
 #ifdef __cplusplus
 }
 #endif

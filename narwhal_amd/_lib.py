@@ -57,6 +57,9 @@ _SIGS = {
                                                  ctypes.c_void_p]),
     "nwc_sanitize_messages": (ctypes.c_int, [_c_u8p, _c_u8p, ctypes.c_size_t, ctypes.c_uint64, _c_u8p, _c_u8p,
                                              _c_u8p, _c_u8p]),
+    "nwc_shard_bounds": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "nwc_cert_cuts": (ctypes.c_int, [_c_u8p, ctypes.c_size_t, ctypes.c_uint32, _c_u8p]),
 }
 
 _lib = None

@@ -1173,7 +1173,10 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
     const u32 fl = cm.flags[kk];
     const bool flags_ok = key >= 0 && sc_lt_l(sw) && key_flags_ok(fl, a.strict != 0) && sh_rok;
     const bool eq = fe_is_zero(fe_sub(sum.X, fe_mul(sh_rx, sum.Z))) && fe_is_zero(fe_sub(sum.Y, fe_mul(sh_ry, sum.Z)));
-    if (key < 0) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;
+    if (key < 0) {
+      if (ca.list) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;
+      else atomicOr(ca.count, 1u);   // latency launch: flag it, the host re-runs the general path
+    }
     if (flags_ok && eq) atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));
   }
 }

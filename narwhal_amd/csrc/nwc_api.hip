@@ -301,12 +301,15 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const VPath path = verify_path();
   const bool comb = path == VPath::Default && d.cm_n && d.cm_comb;
   if (comb && n <= NWC_WIDE_MAX && (flags & LV_ALL_CACHED)) {
-    // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none)
+    // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none).
+    // The host checked every key against its view of the cache (set under g_cm_mu, like the
+    // devices'); should a key still be missing on the device, the kernel sets the word after the
+    // verdict words instead of listing it, and the caller re-runs the general path.
     const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
     const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base16,
                             d.scratch, d.fb_list, d.fb_count, 0u, cm};
-    const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
-    if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
+    const nwc::CombArgs ca{nullptr, reinterpret_cast<uint32_t*>(out_words + (n + 63) / 64), d.comb_base, d.comb16};
+    if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64 + 1), s));
     hipLaunchKernelGGL(nwc::k_verify_comb_wide, dim3((unsigned)n), dim3(128), 0, s, a, ca);
     HIP_TRY(hipGetLastError());
     return 0;
@@ -417,16 +420,17 @@ int launch_cert_reduce(const uint64_t* leaf, const uint32_t* offs, uint64_t m, u
   return 0;
 }
 
-// Run fn(device_index, lo, hi) over [0, n) split across all devices, one host thread each.
+// Run fn(device_index, lo, hi) over [0, n) split across all devices, one host thread each.  The
+// ranges come from nwc_shard_bounds: every range but the last starts on a multiple of 64 units.
 template <class F>
 int shard(uint64_t n, F fn) {
   const int nd = (int)g_devs.size();
   if (nd == 1 || n < 4096) return fn(0, (uint64_t)0, n);
   std::vector<int> rc(nd, 0);
   std::vector<std::thread> th;
-  const uint64_t per = (n + nd - 1) / nd;
   for (int i = 0; i < nd; ++i) {
-    const uint64_t lo = std::min<uint64_t>(n, (uint64_t)i * per), hi = std::min<uint64_t>(n, lo + per);
+    uint64_t lo = 0, hi = 0;
+    nwc_shard_bounds(n, (uint32_t)nd, (uint32_t)i, &lo, &hi);
     th.emplace_back([&, i, lo, hi] {
       rc[i] = fn(i, lo, hi);
     });
@@ -469,14 +473,14 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
   if (n == 0) return 0;
   const uint64_t msg_bytes = msg_index ? 32 * nmsgs : (msg_stride ? 32 * n : 32);
   const size_t need = align256(msg_bytes) + align256(msg_index ? 4 * n : 0) + align256(32 * n) + align256(64 * n) +
-                      align256(8 * words);
+                      align256(8 * (words + 1));
   if (int rc = d.ensure_arena(need)) return rc;
   Carve c(d.arena);
   uint8_t* dm = c.take<uint8_t>(msg_bytes);
   uint32_t* dmi = msg_index ? c.take<uint32_t>(4 * n) : nullptr;
   uint8_t* dp = c.take<uint8_t>(32 * n);
   uint8_t* ds = c.take<uint8_t>(64 * n);
-  uint64_t* dout = c.take<uint64_t>(8 * words);
+  uint64_t* dout = c.take<uint64_t>(8 * (words + 1));   // + the latency kernel's missing-key word
   if (need <= NWC_PINNED_STAGE_MAX) {
     // small call (a certificate, a header): pack into pinned memory, one H2D, one D2H
     if (int rc = d.ensure_pinned(NWC_PINNED_STAGE_MAX)) return rc;
@@ -485,13 +489,19 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     if (msg_index) std::memcpy(h + ((uint8_t*)dmi - d.arena), msg_index + lo, 4 * n);
     std::memcpy(h + (dp - d.arena), pks + 32 * lo, 32 * n);
     std::memcpy(h + (ds - d.arena), sigs + 64 * lo, 64 * n);
-    std::memset(h + ((uint8_t*)dout - d.arena), 0, 8 * words);
-    HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena) + 8 * words, hipMemcpyHostToDevice,
+    std::memset(h + ((uint8_t*)dout - d.arena), 0, 8 * (words + 1));
+    HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena) + 8 * (words + 1), hipMemcpyHostToDevice,
                            d.stream));
     const int fl = LV_OUT_ZEROED | (d.cm_n && g_hcm.all_cached(pks + 32 * lo, n) ? LV_ALL_CACHED : 0);
     if (int rc = launch_verify(d, dm, dmi, msg_stride ? 1 : 0, dp, ds, n, strict, dout, d.stream, fl)) return rc;
-    HIP_TRY(hipMemcpyAsync(h, dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipMemcpyAsync(h, dout, 8 * (words + 1), hipMemcpyDeviceToHost, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
+    if ((fl & LV_ALL_CACHED) && h[8 * words] != 0) {
+      // a key was missing on the device after all: the general path decides every equation
+      if (int rc = launch_verify(d, dm, dmi, msg_stride ? 1 : 0, dp, ds, n, strict, dout, d.stream)) return rc;
+      HIP_TRY(hipMemcpyAsync(h, dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
+      HIP_TRY(hipStreamSynchronize(d.stream));
+    }
     std::memcpy(out_words.data(), h, 8 * words);
     return 0;
   }
@@ -513,6 +523,28 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
 
 extern "C" {
 
+int nwc_shard_bounds(uint64_t n, uint32_t world, uint32_t rank, uint64_t* lo, uint64_t* hi) {
+  if (!lo || !hi || world == 0 || rank >= world) return set_err(NWC_ERR_ARG, "bad shard arguments");
+  const uint64_t words = (n + 63) / 64, per = (words + world - 1) / world;
+  *lo = std::min<uint64_t>(n, (uint64_t)rank * per * 64);
+  *hi = std::min<uint64_t>(n, ((uint64_t)rank + 1) * per * 64);
+  return 0;
+}
+
+int nwc_cert_cuts(const uint32_t* offsets, size_t m, uint32_t world, uint64_t* cuts) {
+  if (!offsets || !cuts || world == 0) return set_err(NWC_ERR_ARG, "bad cut arguments");
+  const uint64_t nv = offsets[m];
+  cuts[0] = 0;
+  size_t c = 0;
+  for (uint32_t r = 1; r < world; ++r) {
+    const uint64_t target = nv * r / world;
+    while (c < m && offsets[c] < target) ++c;   // first boundary at or past the target
+    cuts[r] = offsets[c];
+  }
+  cuts[world] = nv;
+  return 0;
+}
+
 int nwc_version(void) { return (1 << 16) | 0; }
 
 const char* nwc_last_error(void) { return t_err.c_str(); }
@@ -533,6 +565,18 @@ int nwc_init(uint32_t device_mask) {
     g_devs.push_back(std::move(d));
   }
   if (g_devs.empty()) return set_err(NWC_ERR_NO_DEVICE, "device mask 0x%x selects no visible device", device_mask);
+  // Test hook: NWC_VIRTUAL_DEVICES=k opens k contexts (own stream, tables, buffers) on a single
+  // selected GPU, so the multi-device host paths -- shard threads, certificate cuts, bitmap
+  // merges -- run for real on a one-GPU box (tests/test_gpu_multidev.py).
+  const char* ve = std::getenv("NWC_VIRTUAL_DEVICES");
+  const int virt = ve ? std::atoi(ve) : 0;
+  const bool single = g_devs.size() == 1;
+  for (int k = 1; single && k < virt && k < 32; ++k) {
+    auto d = std::make_unique<DevCtx>();
+    d->hip_id = g_devs[0]->hip_id;
+    if (int rc = init_device(*d)) { g_devs.clear(); return rc; }
+    g_devs.push_back(std::move(d));
+  }
   return 0;
 }
 
@@ -578,13 +622,17 @@ int nwc_verify_strict_many(const uint8_t* msgs32, const uint8_t* pks, const uint
                            uint8_t* verdict_bitmap) {
   if (int rc = require_init()) return rc;
   if (n && (!msgs32 || !pks || !sigs || !verdict_bitmap)) return set_err(NWC_ERR_ARG, "null buffer");
-  return shard(n, [&](int di, uint64_t lo, uint64_t hi) -> int {
-    std::vector<uint64_t> words;
-    int rc = verify_range(di, msgs32, 1, nullptr, pks, sigs, lo, hi, 1, words, 0);
-    if (rc) return rc;
-    merge_bits(verdict_bitmap, lo, words, hi - lo);
-    return 0;
-  });
+  // per-device verdict words are merged into the caller's bitmap on this thread, after the join
+  std::vector<std::vector<uint64_t>> parts(g_devs.size());
+  std::vector<std::pair<uint64_t, uint64_t>> range(g_devs.size(), {0, 0});
+  if (int rc = shard(n, [&](int di, uint64_t lo, uint64_t hi) -> int {
+        range[di] = {lo, hi};
+        return verify_range(di, msgs32, 1, nullptr, pks, sigs, lo, hi, 1, parts[di], 0);
+      }))
+    return rc;
+  for (size_t di = 0; di < parts.size(); ++di)
+    if (range[di].second > range[di].first) merge_bits(verdict_bitmap, range[di].first, parts[di], range[di].second - range[di].first);
+  return 0;
 }
 
 int nwc_verify_strict(const uint8_t msg32[32], const uint8_t pk[32], const uint8_t sig[64]) {
@@ -629,14 +677,8 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
   std::vector<uint64_t> leaf((nv + 63) / 64, 0);
   // shard votes on certificate boundaries
   const int nd = (int)g_devs.size();
-  std::vector<uint64_t> cuts{0};
-  for (int i = 1; i < nd; ++i) {
-    uint64_t target = nv * i / nd;
-    size_t c = 0;
-    while (c < m && offsets[c] < target) ++c;
-    cuts.push_back(offsets[c]);
-  }
-  cuts.push_back(nv);
+  std::vector<uint64_t> cuts(nd + 1);
+  nwc_cert_cuts(offsets, m, (uint32_t)nd, cuts.data());
   std::vector<int> rc(nd, 0);
   std::vector<std::vector<uint64_t>> parts(nd);
   std::vector<std::thread> th;
@@ -664,7 +706,17 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
   return 0;
 }
 
+// Committee updates are serialised: the devices' caches and the host's view of them (g_hcm, which
+// the latency path trusts) change together, one committee at a time.
+std::mutex g_cm_mu;
+static int set_committee_locked(const uint8_t* pks, size_t n);
+
 int nwc_set_committee(const uint8_t* pks, size_t n) {
+  std::lock_guard<std::mutex> lk(g_cm_mu);
+  return set_committee_locked(pks, n);
+}
+
+static int set_committee_locked(const uint8_t* pks, size_t n) {
   if (int rc = require_init()) return rc;
   if (n && !pks) return set_err(NWC_ERR_ARG, "null buffer");
   if (n > (1u << 20)) return set_err(NWC_ERR_ARG, "committee of %zu keys is too large", n);
@@ -882,9 +934,35 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
     if (worker_offsets[k + 1] < worker_offsets[k]) return set_err(NWC_ERR_ARG, "worker_offsets not monotone");
   const uint32_t nw = n ? worker_offsets[n] : 0;
   if (nw && !worker_ids) return set_err(NWC_ERR_ARG, "null worker ids");
-  // the key cache indexes authorities by their position in `pks` (a duplicate key keeps its
-  // first position, as the committee's BTreeMap would hold one entry)
-  if (int rc = nwc_set_committee(pks, n)) return rc;
+  // config::Committee holds a BTreeMap<PublicKey, Authority>: a key listed twice is one authority
+  // with the LAST entry's stake and workers (a map insert replaces the value).  Deduplicate so the
+  // cache index, the stake table and the quorum (config/src/lib.rs:181-186) all see that map.
+  std::vector<uint8_t> ukeys;
+  std::vector<uint64_t> ustakes;
+  std::vector<uint32_t> uoff{0}, uids;
+  {
+    std::vector<size_t> last;   // entry index of the last occurrence, in first-appearance order
+    for (size_t k = 0; k < n; ++k) {
+      size_t j = 0;
+      while (j < last.size() && std::memcmp(pks + 32 * last[j], pks + 32 * k, 32) != 0) ++j;
+      if (j == last.size()) last.push_back(k);
+      else last[j] = k;
+    }
+    for (size_t k : last) {
+      ukeys.insert(ukeys.end(), pks + 32 * k, pks + 32 * k + 32);
+      ustakes.push_back(stakes[k]);
+      if (worker_offsets[k + 1] > worker_offsets[k])
+        uids.insert(uids.end(), worker_ids + worker_offsets[k], worker_ids + worker_offsets[k + 1]);
+      uoff.push_back((uint32_t)uids.size());
+    }
+  }
+  n = ustakes.size();
+  pks = ukeys.data();
+  stakes = ustakes.data();
+  worker_offsets = uoff.data();
+  worker_ids = uids.data();
+  std::lock_guard<std::mutex> cm_lk(g_cm_mu);
+  if (int rc = set_committee_locked(pks, n)) return rc;
   uint64_t total = 0;
   for (size_t k = 0; k < n; ++k) total += stakes[k];
   for (auto& dp : g_devs) {
@@ -904,7 +982,7 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
     if (n) {
       HIP_TRY(hipMemcpy(d.cc_stakes, stakes, 8 * n, hipMemcpyHostToDevice));
       HIP_TRY(hipMemcpy(d.cc_worker_off, worker_offsets, 4 * (n + 1), hipMemcpyHostToDevice));
-      if (nw) HIP_TRY(hipMemcpy(d.cc_worker_ids, worker_ids, 4 * (size_t)nw, hipMemcpyHostToDevice));
+      if (!uids.empty()) HIP_TRY(hipMemcpy(d.cc_worker_ids, worker_ids, 4 * uids.size(), hipMemcpyHostToDevice));
     }
     d.cc_n = (uint32_t)n;
   }

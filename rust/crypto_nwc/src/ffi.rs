@@ -1,0 +1,50 @@
+//! Raw declarations of every entry point of include/nwc.h (checked against the header by
+//! tests/test_rust_shim.py: same names, same parameter types, same order).
+#![allow(dead_code)]
+use std::os::raw::{c_char, c_int, c_void};
+
+#[link(name = "nwc")]
+extern "C" {
+    pub fn nwc_init(device_mask: u32) -> c_int;
+    pub fn nwc_shutdown();
+    pub fn nwc_last_error() -> *const c_char;
+    pub fn nwc_version() -> c_int;
+    pub fn nwc_device_count() -> c_int;
+
+    pub fn nwc_verify_strict(msg32: *const u8, pk: *const u8, sig: *const u8) -> c_int;
+    pub fn nwc_verify_batch(msg32: *const u8, pks: *const u8, sigs: *const u8, n: usize, bad_bitmap: *mut u8) -> c_int;
+    pub fn nwc_verify_strict_many(msgs32: *const u8, pks: *const u8, sigs: *const u8, n: usize,
+                                  verdict_bitmap: *mut u8) -> c_int;
+    pub fn nwc_verify_batch_many(digests: *const u8, offsets: *const u32, pks: *const u8, sigs: *const u8, m: usize,
+                                 cert_ok_bitmap: *mut u8, bad_vote_bitmap: *mut u8) -> c_int;
+    pub fn nwc_set_committee(pks: *const u8, n: usize) -> c_int;
+
+    pub fn nwc_set_committee_config(pks: *const u8, stakes: *const u64, n: usize, worker_offsets: *const u32,
+                                    worker_ids: *const u32) -> c_int;
+    pub fn nwc_sanitize_messages(data: *const u8, offsets: *const u64, m: usize, gc_round: u64, vote_target: *const u8,
+                                 codes: *mut i32, digests32: *mut u8, kinds: *mut u8) -> c_int;
+    pub fn nwc_dev_sanitize_messages(d_data: *const c_void, d_offsets: *const c_void, m: u64, total: u64, gc_round: u64,
+                                     vote_target: *const u8, d_codes: *mut c_void, d_digests32: *mut c_void,
+                                     stream: *mut c_void) -> c_int;
+
+    pub fn nwc_digest32(data: *const u8, len: usize, out32: *mut u8) -> c_int;
+    pub fn nwc_sha512_trunc32_many(data: *const u8, offsets: *const u64, n: usize, out32: *mut u8) -> c_int;
+
+    pub fn nwc_dev_verify(d_msgs: *const c_void, d_msg_index: *const c_void, msg_stride: u64, d_pks: *const c_void,
+                          d_sigs: *const c_void, n: u64, strict: c_int, d_verdict_words: *mut c_void,
+                          stream: *mut c_void) -> c_int;
+    pub fn nwc_dev_cert_reduce(d_leaf_words: *const c_void, d_offsets: *const c_void, m: u64, nvotes: u64,
+                               d_cert_words: *mut c_void, d_bad_words: *mut c_void, stream: *mut c_void) -> c_int;
+    pub fn nwc_dev_sha512_trunc32(d_data: *const c_void, d_offsets: *const c_void, n: u64, d_out32: *mut c_void,
+                                  stream: *mut c_void) -> c_int;
+    pub fn nwc_dev_sha512_trunc32_ranges(d_data: *const c_void, d_starts: *const c_void, d_ends: *const c_void, n: u64,
+                                         d_out32: *mut c_void, stream: *mut c_void) -> c_int;
+    pub fn nwc_dev_derive32(tag: *const u8, taglen: c_int, first: u64, n: u64, d_out: *mut c_void,
+                            stream: *mut c_void) -> c_int;
+    pub fn nwc_dev_keygen_sign(d_seeds: *const c_void, d_msgs: *const c_void, n: u64, d_pks: *mut c_void,
+                               d_sigs: *mut c_void, stream: *mut c_void) -> c_int;
+    pub fn nwc_dev_set_device(device: c_int) -> c_int;
+
+    pub fn nwc_shard_bounds(n: u64, world: u32, rank: u32, lo: *mut u64, hi: *mut u64) -> c_int;
+    pub fn nwc_cert_cuts(offsets: *const u32, m: usize, world: u32, cuts: *mut u64) -> c_int;
+}

@@ -1,0 +1,85 @@
+//! `crypto_nwc`: the device side of Narwhal's `crypto` crate (/root/reference/crypto/src/lib.rs).
+//!
+//! The reference crate keeps its types and API; its verification bodies forward here
+//!:
+//!
+//! ```ignore
+//! // crypto/src/lib.rs:200-204  Signature::verify
+//! pub fn verify(&self, digest: &Digest, public_key: &PublicKey) -> Result<(), CryptoError> {
+//!     if crypto_nwc::verify_strict(&digest.0, &public_key.0, &self.flatten()) { Ok(()) }
+//!     else { Err(CryptoError::new()) }
+//! }
+//! // crypto/src/lib.rs:206-219  Signature::verify_batch
+//! pub fn verify_batch<'a, I>(digest: &Digest, votes: I) -> Result<(), CryptoError>
+//! where I: IntoIterator<Item = &'a (PublicKey, Signature)> {
+//!     let (pks, sigs): (Vec<[u8; 32]>, Vec<[u8; 64]>) =
+//!         votes.into_iter().map(|(k, s)| (k.0, s.flatten())).unzip();
+//!     if crypto_nwc::verify_batch(&digest.0, &pks, &sigs) { Ok(()) } else { Err(CryptoError::new()) }
+//! }
+//! // worker/src/processor.rs:38
+//! let digest = Digest(crypto_nwc::digest32(&batch));
+//! ```
+//!
+//! Return convention of the C ABI: 0 = valid, 1 = invalid, < 0 = device/runtime failure, which
+//! is never reported as an invalid signature -- these wrappers panic on it, as the crate's
+//! callers have no error path for a broken device.
+mod ffi;
+
+pub use ffi::*;
+
+use std::ffi::CStr;
+use std::os::raw::c_int;
+use std::sync::Once;
+
+static INIT: Once = Once::new();
+
+/// `nwc_init(device_mask)` once per process (node start-up, node/src/main.rs:69-134).  Later
+/// calls are no-ops; the wrappers below call it with mask 0 (device 0) if nobody did.
+pub fn init(device_mask: u32) {
+    INIT.call_once(|| {
+        let rc = unsafe { ffi::nwc_init(device_mask) };
+        check(rc);
+    });
+}
+
+fn check(rc: c_int) -> bool {
+    if rc < 0 {
+        let msg = unsafe { CStr::from_ptr(ffi::nwc_last_error()) };
+        panic!("libnwc failure {}: {}", rc, msg.to_string_lossy());
+    }
+    rc == 0
+}
+
+/// `Signature::verify` = dalek `verify_strict` (crypto/src/lib.rs:200-204).
+pub fn verify_strict(digest: &[u8; 32], public_key: &[u8; 32], signature: &[u8; 64]) -> bool {
+    init(0);
+    check(unsafe { ffi::nwc_verify_strict(digest.as_ptr(), public_key.as_ptr(), signature.as_ptr()) })
+}
+
+/// `Signature::verify_batch` = dalek `verify_batch` over one digest (crypto/src/lib.rs:206-219).
+/// An empty batch is valid.
+pub fn verify_batch(digest: &[u8; 32], public_keys: &[[u8; 32]], signatures: &[[u8; 64]]) -> bool {
+    assert_eq!(public_keys.len(), signatures.len());
+    init(0);
+    let pks: Vec<u8> = public_keys.iter().flat_map(|k| k.iter().copied()).collect();
+    let sigs: Vec<u8> = signatures.iter().flat_map(|s| s.iter().copied()).collect();
+    check(unsafe {
+        ffi::nwc_verify_batch(digest.as_ptr(), pks.as_ptr(), sigs.as_ptr(), public_keys.len(), std::ptr::null_mut())
+    })
+}
+
+/// `Sha512::digest(bytes)[..32]` (worker/src/processor.rs:38).
+pub fn digest32(data: &[u8]) -> [u8; 32] {
+    init(0);
+    let mut out = [0u8; 32];
+    check(unsafe { ffi::nwc_digest32(data.as_ptr(), data.len(), out.as_mut_ptr()) });
+    out
+}
+
+/// The committee's keys (config/src/lib.rs:154-156), cached on the devices.  Optional: verdicts
+/// never depend on it.
+pub fn set_committee(public_keys: &[[u8; 32]]) {
+    init(0);
+    let pks: Vec<u8> = public_keys.iter().flat_map(|k| k.iter().copied()).collect();
+    check(unsafe { ffi::nwc_set_committee(pks.as_ptr(), public_keys.len()) });
+}

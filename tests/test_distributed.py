@@ -87,3 +87,47 @@ def test_two_rank_gloo_verdict_allgather(oracle):
         assert pr.exitcode == 0
     assert (merged == expect).all()
     assert mx == 2.0
+
+
+# ---- the library's own cut logic (nwc_shard_bounds / nwc_cert_cuts: the C++ that the host entry
+# points use to split work over the devices of the init mask), against the Python twin above.
+def _lib():
+    from narwhal_amd import _lib as L
+    return L, L.load(init=False)
+
+
+def test_c_shard_bounds_match_python():
+    import ctypes
+    L, lib = _lib()
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    for n in (0, 1, 63, 64, 65, 4095, 4096, 4097, 1000, 1 << 20, 64 * 1024 * 1024 + 5):
+        for world in (1, 2, 3, 4, 7, 8):
+            prev = 0
+            for r in range(world):
+                assert lib.nwc_shard_bounds(n, world, r, ctypes.byref(lo), ctypes.byref(hi)) == 0
+                assert (lo.value, hi.value) == shard.shard_bounds(n, world, r), (n, world, r)
+                assert lo.value == prev and (lo.value % 64 == 0 or lo.value == n)   # whole verdict bytes
+                prev = hi.value
+            assert prev == n
+    assert lib.nwc_shard_bounds(10, 0, 0, ctypes.byref(lo), ctypes.byref(hi)) == L.NWC_ERR_ARG
+    assert lib.nwc_shard_bounds(10, 2, 2, ctypes.byref(lo), ctypes.byref(hi)) == L.NWC_ERR_ARG
+
+
+def test_c_cert_cuts_match_python():
+    L, lib = _lib()
+    rng = np.random.default_rng(1)
+    layouts = [np.zeros(1, np.int64),                                   # m = 0
+               np.array([0, 0, 0, 0]),                                  # only empty certificates
+               np.array([0, 67]),                                       # one certificate, m < devices
+               np.array([0, 5, 5, 9]),                                  # m < devices, an empty one
+               np.concatenate([[0], np.cumsum(rng.integers(0, 90, 500))]),
+               np.concatenate([[0], np.cumsum(np.where(rng.random(300) < 0.3, 0, 67))])]
+    for offs in layouts:
+        m = len(offs) - 1
+        o32 = np.ascontiguousarray(offs, dtype=np.uint32)
+        for world in (1, 2, 3, 4, 8):
+            cuts = np.zeros(world + 1, np.uint64)
+            assert lib.nwc_cert_cuts(L.buf(o32), m, world, L.buf(cuts)) == 0
+            assert cuts.tolist() == shard.cert_cuts(offs, world), (m, world)
+            assert set(cuts.tolist()) <= set(offs.tolist())
+            assert cuts[0] == 0 and cuts[-1] == offs[-1] and (np.diff(cuts.astype(np.int64)) >= 0).all()
