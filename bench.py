@@ -45,9 +45,13 @@ W_S, W_M, W_SHA = 1546, 1429, 1
 # Frozen at the round-1 build (tools/count_ops.py on commit dc19643, before any kernel tuning):
 # later speedups of fe_mul/fe_sq must raise `frac`, not shrink the work they are measured against.
 OPS_S, OPS_M, OPS_SHA = 134, 167, 5039
-# int-VALU issue peak: 64 lane-instructions / clk / CU for VOP3-class ops (v_mad_u64_u32,
-# v_mad_i64_i32, v_alignbit, v_bitop3 ...; tools/microbench/int_rates.hip) x 256 CU x 2.4 GHz
-VALU_PEAK_TOPS = 64 * 256 * 2.4e9 / 1e12      # 39.32 T lane-ops/s
+# VALU issue peak (MI355X_MICROARCH.md "Execution model": a wave64 VALU instruction issues over 2
+# cycles on a SIMD-32 -> 128 lane-instructions / clk / CU) x 256 CU x 2.4 GHz.
+VALU_PEAK_TOPS = 128 * 256 * 2.4e9 / 1e12     # 78.64 T lane-ops/s
+# The measured issue rate of the VOP3 integer class that dominates these kernels
+# (v_mad_i64_i32 / v_mad_u64_u32, v_alignbit, v_bitop3, v_lshl_add_u64: 4 cycles per wave64
+# instruction at full occupancy; tools/microbench/int_rates.hip, profiles/r02/microbench/)
+VOP3_RATE_TOPS = 64 * 256 * 2.4e9 / 1e12      # 39.32 T lane-ops/s
 HBM_PEAK_GBS = 8000.0                          # MI355X_MICROARCH.md (spec)
 
 CFG4_TXS, CFG4_TX_BYTES = 977, 512
@@ -55,7 +59,7 @@ CFG4_BATCH_BYTES = 12 + CFG4_TXS * (8 + CFG4_TX_BYTES)   # 508,052
 CFG4_STRIDE = (CFG4_BATCH_BYTES + 255) & ~255
 
 
-PROFILE_ROUND = "r01"   # profiles/<round>/summary.json: rocprofv3 PMC passes of this build
+PROFILE_ROUND = "r02"   # profiles/<round>/summary.json: rocprofv3 PMC passes of this build
 
 
 def profile_counters(*kernel_names: str):
@@ -70,8 +74,8 @@ def profile_counters(*kernel_names: str):
     for k in kernel_names:
         d = summ.get(k, {})
         if "hbm_traffic_bytes_per_launch" in d:
-            return {"traffic": d["hbm_traffic_bytes_per_launch"], "valu_issue_frac": d.get("valu_issue_frac"),
-                    "valu_insts_per_wave": d.get("valu_insts_per_lane"), "avg_ns": d.get("avg_ns"),
+            return {"traffic": d["hbm_traffic_bytes_per_launch"], "valu_insts_per_lane": d.get("valu_insts_per_lane"),
+                    "lane_ops_per_launch": d.get("SQ_INSTS_VALU", 0) * 64, "avg_ns": d.get("avg_ns"),
                     "source": "profiles/%s/summary.json (%s)" % (PROFILE_ROUND, k)}
     return None
 
@@ -192,17 +196,20 @@ def bench_cfg1(lib, calls: int = 10000, cpu_baseline: bool = False):
         if cache:
             _lib.check(lib.nwc_set_committee(_lib.buf(committee), n + 1))
         lat = []
+        first_us = None
         for i in range(calls + 50):
             t0 = time.perf_counter()
             rc = lib.nwc_verify_batch(_lib.buf(d), _lib.buf(p), _lib.buf(s), n, None)
             dt = time.perf_counter() - t0
             assert rc == 0, rc
+            if i == 0:
+                first_us = dt * 1e6   # uncached keys: includes their torsion test (then memoised)
             if i >= 50:
                 lat.append(dt)
         if cache:
             _lib.check(lib.nwc_set_committee(None, 0))
         lat = np.array(lat) * 1e6
-        out[tag] = {"calls": calls, "p50_us": float(np.percentile(lat, 50)),
+        out[tag] = {"calls": calls, "first_call_us": first_us, "p50_us": float(np.percentile(lat, 50)),
                     "p99_us": float(np.percentile(lat, 99)), "calls_per_s": float(1e6 / lat.mean())}
     if cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_cfg1(d, p, s, n, min(calls, 2000))
@@ -250,7 +257,7 @@ def cpu_baseline_cfg3(cdig, pks, sigs, m: int, Q: int, bad, budget_s: float):
         k = min(m, int(k * max(2.0, budget_s / max(dt, 1e-3) * 0.8)))
     exp = ~bad[:k * Q].view(k, Q).any(dim=1).cpu().numpy()
     return {"value": k * Q / dt, "unit": "votes/s", "certs_per_s": k / dt, "cores": th, "kind": "port",
-            "parity_ok": bool((got == exp).all()),
+            "value_per_thread": k * Q / dt / th, "parity_ok": bool((got == exp).all()),
             "sample": "%d of the cfg-3 certificates (dalek verify_batch algorithm: random z, Straus MSM; "
                       "C restatement, %d threads, %.1f s)" % (k, th, dt)}
 
@@ -326,6 +333,10 @@ def make_cfg3_wire(m: int, N: int = 100, Q: int = 67):
     voters = np.argsort(rng.random((m, N)), axis=1)[:, :Q]
     rounds = (np.arange(m, dtype=np.uint64) % 1000) + 1
     parents = rng.integers(0, 256, (m, Q, 32), dtype=np.uint8)
+    # Header.parents is a BTreeSet<Digest>: serialised in ascending byte order (what every honest
+    # encoder sends; the GPU decoder canonicalises any other order before Header::digest)
+    order = np.lexsort(parents.transpose(2, 0, 1)[::-1], axis=-1)
+    parents = np.take_along_axis(parents, order[:, :, None], axis=1)
     ids = np.empty((m, 32), np.uint8)
     cdig = np.empty((m, 32), np.uint8)
     for c in range(m):
@@ -471,26 +482,59 @@ def bench_cfg5(lib, rank: int, world: int, total: int, steps: int):
             "edge_slots_per_gpu": int(slot.numel()), "parity_ok": bool(okt.item() == 1)}
 
 
-# ---- timing ----------------------------------------------------------------------------------
-def timed_kernel(fn, iters: int):
-    """Average duration (ms) of fn() launches measured with HIP events on torch's current
-    stream (the stream the library launches on)."""
-    import torch
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / iters
-
-
+# ---- host ------------------------------------------------------------------------------------
 def cpu_threads() -> int:
+    """Every host CPU this process may use: the affinity mask, capped by the cgroup's CPU quota
+    (on the GPU box: 16 CPUs of a 2 x 64-core host; OMP_NUM_THREADS says the same)."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    q = cgroup_cpus()
+    if q:
+        n = min(n, q)
+    return max(1, n)
+
+
+def cgroup_cpus():
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_info():
+    """the CPU model and core counts next to every CPU baseline."""
+    model = "?"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    phys = set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" in line:
+                k, v = (x.strip() for x in line.split(":", 1))
+                cur[k] = v
+            elif cur:
+                phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    return {"cpu_model": model, "logical_cpus": os.cpu_count(), "physical_cores": len(phys) or None,
+            "affinity_cpus": aff, "cgroup_cpu_quota": cgroup_cpus(), "nproc": int(os.popen("nproc").read() or 0),
+            "threads_used": cpu_threads()}
 
 
 def cpu_baseline_verify(msgs, pks, sigs, budget_s: float):
@@ -508,8 +552,10 @@ def cpu_baseline_verify(msgs, pks, sigs, budget_s: float):
     v = orc.strict_many(m[:n], p[:n], s[:n], th)
     dt = time.perf_counter() - t0
     assert v.all(), "oracle rejected a valid signature"
-    return {"value": n / dt, "unit": "verifies/s", "cores": th, "kind": "port",
-            "sample": "%d of the cfg-2 triples (C restatement of dalek verify_strict, %d threads, %.1f s)" % (n, th, dt)}
+    return {"value": n / dt, "unit": "verifies/s", "cores": th, "kind": "port", "value_per_thread": n / dt / th,
+            "host": host_info(),
+            "sample": "%d of the cfg-2 triples (C restatement of dalek verify_strict, %d threads = every CPU the "
+                      "box grants this process, %.1f s)" % (n, th, dt)}
 
 
 def cpu_baseline_digest(budget_s: float):
@@ -529,6 +575,7 @@ def cpu_baseline_digest(budget_s: float):
             break
     dt = time.perf_counter() - t0
     out = {"value": reps * len(blob) / dt / 1e9, "unit": "GB/s", "cores": th, "kind": "port",
+           "value_per_thread": reps * len(blob) / dt / 1e9 / th,
            "sample": "%d x %d cfg-4 batches (C restatement SHA-512, %d threads, %.1f s)" % (reps, nb, th, dt)}
     out["openssl"] = cpu_digest_openssl(blob, nb, th, budget_s / 2)
     return out
@@ -552,6 +599,33 @@ def cpu_digest_openssl(blob: bytes, nb: int, th: int, budget_s: float):
         dt = time.perf_counter() - t0
     return {"value": reps * nb * CFG4_BATCH_BYTES / dt / 1e9, "unit": "GB/s", "cores": th, "kind": "openssl",
             "parity_ok": ok, "sample": "%d x %d cfg-4 batches (hashlib/OpenSSL SHA-512, %d threads, %.1f s)" % (reps, nb, th, dt)}
+
+
+def roofline_verify(vpc, n: int, kernel_ms: float, effective_tops: float):
+    """k_verify's roofline entry.  achieved = the VALU lane-instructions one launch issues (this
+    build's SQ_INSTS_VALU x 64 from the committed rocprofv3 pass, profiles/<round>/summary.json)
+    over the launch's duration measured live with HIP events; peak = the guide's VALU issue rate.
+    frac_vop3_rate relates it to the measured 4-cycle issue of the VOP3 integer class the kernel
+    consists of; effective_frac prices the dalek work model (W_strict) instead of the instructions
+    actually issued (the half-size ladder issues fewer, so it can exceed the hardware fraction)."""
+    out = {"bound": "valu", "unit": "T lane-ops/s", "peak": VALU_PEAK_TOPS, "kernel": "k_verify",
+           "kernel_ms": kernel_ms, "verifies_per_launch": n,
+           "peak_source": "MI355X_MICROARCH.md: wave64 VALU issue 2 cycles/SIMD x 4 SIMD x 256 CU x 2.4 GHz",
+           "effective_frac": effective_tops / VALU_PEAK_TOPS,
+           "work_model": "%d S + %d M + %d SHA-512 block per verify (dalek op model) x (%d, %d, %d) lane-ops"
+                         % (W_S, W_M, W_SHA, OPS_S, OPS_M, OPS_SHA)}
+    if vpc:
+        ach = vpc["lane_ops_per_launch"] / (kernel_ms * 1e-3) / 1e12
+        out.update({"achieved": ach, "frac": ach / VALU_PEAK_TOPS, "frac_vop3_rate": ach / VOP3_RATE_TOPS,
+                    "valu_insts_per_verify": vpc["valu_insts_per_lane"],
+                    "traffic": vpc["traffic"], "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
+                    "traffic_per_verify": vpc["traffic"] / n, "algorithmic_bytes_per_verify": 128,
+                    "traffic_over_algorithmic": vpc["traffic"] / (128.0 * n),
+                    "rocprof_avg_ms": vpc["avg_ns"] * 1e-6, "pmc_source": vpc["source"]})
+    else:
+        out.update({"achieved": None, "frac": None, "traffic": None,
+                    "pmc_source": "profiles/%s/summary.json missing" % PROFILE_ROUND})
+    return out
 
 
 # ---- main ------------------------------------------------------------------------------------
@@ -584,15 +658,19 @@ def main():
     run = lambda: device.verify(msgs, pks, sigs, strict=True, out=words)  # noqa: E731
     for _ in range(args.warmup):
         run()
+    # HIP events around every step, on the stream the library launches on (torch's current
+    # stream), recorded inside the same timed loop as the wall clock
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     barrier(world)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for e0, e1 in evs:
+        e0.record()
         run()
+        e1.record()
     barrier(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
     ok = bool(device.unpack_bits(words, n).all())
-    # per-launch kernel time, HIP events on the launch stream
-    kernel_ms = timed_kernel(run, max(3, args.steps))
+    kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)
     # verdict all-gather over RCCL (not needed for correctness; timed separately)
     gather_ms = None
     if world > 1:
@@ -605,7 +683,7 @@ def main():
         gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, world)
         ok = ok and bool(device.unpack_bits(allw, world * words.numel() * 64).all())
     value = world * n * args.steps / dt
-    achieved_tops = n / (kernel_ms * 1e-3) * ops_per_verify() / 1e12
+    effective_tops = n / (kernel_ms * 1e-3) * ops_per_verify() / 1e12
 
     # ---------------- digest leg (cfg 4)
     digest = None
@@ -619,16 +697,20 @@ def main():
         outs = torch.empty((nb, 32), dtype=torch.uint8, device="cuda")
         dig = lambda: device.sha512_trunc32_ranges(data, starts, ends, out=outs)  # noqa: E731
         dig()
+        devs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(args.digest_steps)]
         barrier(world)
         t0 = time.perf_counter()
-        for _ in range(args.digest_steps):
+        for e0, e1 in devs:
+            e0.record()
             dig()
+            e1.record()
         barrier(world)
         ddt = max_over_ranks(time.perf_counter() - t0, world)
+        dk_ms = sum(e0.elapsed_time(e1) for e0, e1 in devs) / len(devs)
         dbytes = world * nb * CFG4_BATCH_BYTES * args.digest_steps
         o = outs[:3].cpu().numpy()
         dok = all(o[b].tobytes() == hashlib.sha512(cfg4_host_batch(b)).digest()[:32] for b in range(3))
-        dk_ms = timed_kernel(dig, 1)
         dk_gbs = nb * CFG4_BATCH_BYTES / (dk_ms * 1e-3) / 1e9
         # launch_digest's choice: McNaughton-scheduled blocks above one wave per SIMD of messages
         cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
@@ -637,7 +719,7 @@ def main():
                   "batches": nb, "batch_bytes": CFG4_BATCH_BYTES, "pool_distinct_batches": pool,
                   "parity_ok": dok, "kernel": dkernel, "kernel_ms": dk_ms, "kernel_GBps": dk_gbs,
                   "hbm_frac": dk_gbs / HBM_PEAK_GBS,
-                  "valu_frac": dk_gbs * 1e9 / 128 * OPS_SHA / (VALU_PEAK_TOPS * 1e12)}
+                  "effective_valu_frac": dk_gbs * 1e9 / 128 * OPS_SHA / (VALU_PEAK_TOPS * 1e12)}
 
     extras = {}
     if args.cfg5_total > 0:
@@ -660,7 +742,9 @@ def main():
     dpc = profile_counters("nwc::" + digest["kernel"]) if digest is not None else None
     if digest is not None and dpc:
         digest["traffic"] = dpc["traffic"]
-        digest["hw_valu_issue_frac"] = dpc["valu_issue_frac"]
+        # counter fraction: this build's VALU lane-ops per launch (PMC) over the live kernel time
+        digest["valu_frac"] = dpc["lane_ops_per_launch"] / (digest["kernel_ms"] * 1e-3) / (VALU_PEAK_TOPS * 1e12)
+        digest["valu_frac_vop3_rate"] = digest["valu_frac"] * VALU_PEAK_TOPS / VOP3_RATE_TOPS
         digest["pmc_source"] = dpc["source"]
     if rank == 0:
         line = {
@@ -673,18 +757,7 @@ def main():
                        "global_batch": world * n, "parallelism": "shard%d" % world,
                        "verdicts_ok": ok, "verdict_allgather_ms": gather_ms,
                        "allgather_needed": False},
-            "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
-                         "frac": achieved_tops / VALU_PEAK_TOPS,
-                         "frac_kind": "effective (dalek work model; the half-size ladder does less work, so >1 "
-                                      "is possible); hw_valu_issue_frac is the counter-measured fraction",
-                         "traffic": vpc["traffic"] if vpc else None,
-                         "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)",
-                         "hw_valu_issue_frac": vpc["valu_issue_frac"] if vpc else None,
-                         "pmc_source": vpc["source"] if vpc else None,
-                         "kernel": "k_verify", "kernel_ms": kernel_ms,
-                         "ops_per_verify": ops_per_verify(),
-                         "work_model": "%d S + %d M + %d SHA-512 block per verify (dalek op model) x "
-                                       "(%d, %d, %d) VALU lane-ops" % (W_S, W_M, W_SHA, OPS_S, OPS_M, OPS_SHA)},
+            "roofline": roofline_verify(vpc, n, kernel_ms, effective_tops),
             "cpu_baseline": cpu,
             "digest": digest,
             "configs": extras,

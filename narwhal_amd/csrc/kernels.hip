@@ -871,6 +871,43 @@ __global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {
 // directly), tests each distinct key once (k_tors_eval: ge_has_torsion), and clears the verdict bit
 // of every equation whose key has torsion (k_tors_apply).  Committees repeat keys, so the distinct
 // count -- and the cost -- is the committee size, not the vote count.
+// A key's torsion is a fixed property, so every evaluated key is also memoised in a per-device
+// table that persists across launches (KeyMemo: open addressing on the exact 32 bytes, bounded
+// probes, never evicted; a full table just stops memoising).  Verdicts do not depend on it: a
+// key found there carries the flag ge_has_torsion computed for exactly those bytes.
+struct KeyMemo {
+  u32* keys;                // slots x 8 words
+  u32* flag;                // per slot: MEMO_EMPTY, or the key's torsion bit (0 / 1)
+  u32 slot_mask;
+};
+constexpr u32 MEMO_EMPTY = 0xFFFFFFFFu, MEMO_BUSY = 0xFFFFFFFEu;
+constexpr int MEMO_MAX_PROBE = 32;
+__device__ __forceinline__ int memo_lookup(const KeyMemo& m, const u32 aw[8]) {
+  if (!m.keys) return -1;
+  u32 h = committee_hash(aw[0], aw[1]) & m.slot_mask;
+  for (int p = 0; p < MEMO_MAX_PROBE; ++p, h = (h + 1) & m.slot_mask) {
+    const u32 f = m.flag[h];
+    if (f == MEMO_EMPTY) return -1;
+    if (f == MEMO_BUSY) continue;
+    u32 d = 0;
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) d |= m.keys[8 * h + k] ^ aw[k];
+    if (d == 0) return (int)f;
+  }
+  return -1;
+}
+__device__ __forceinline__ void memo_insert(const KeyMemo& m, const u32 aw[8], u32 torsion) {
+  if (!m.keys) return;
+  u32 h = committee_hash(aw[0], aw[1]) & m.slot_mask;
+  for (int p = 0; p < MEMO_MAX_PROBE; ++p, h = (h + 1) & m.slot_mask) {
+    if (atomicCAS(&m.flag[h], MEMO_EMPTY, MEMO_BUSY) == MEMO_EMPTY) {
+      _Pragma("unroll") for (int k = 0; k < 8; ++k) m.keys[8 * h + k] = aw[k];
+      __threadfence();
+      atomicExch(&m.flag[h], torsion);
+      return;
+    }
+  }
+}
+
 struct TorsArgs {
   const uint8_t* pks;
   uint64_t* bits;           // the launch's verdict words
@@ -883,6 +920,7 @@ struct TorsArgs {
   uint32_t* nuniq;
   uint32_t* tflag;          // per slot: 1 = the key has torsion
   Committee committee;
+  KeyMemo memo;
 };
 __device__ __forceinline__ bool tors_candidate(const TorsArgs& t, uint64_t idx, uint64_t& i, u32 aw[8], int& key) {
   i = t.list ? (uint64_t)t.list[idx] : idx;
@@ -905,9 +943,9 @@ __global__ __launch_bounds__(256) void k_tors_mark(TorsArgs t) {
     u32 aw[8];
     int key;
     if (!tors_candidate(t, idx, i, aw, key)) continue;
-    if (key >= 0) {
-      if (t.committee.flags[key] & KEY_TORSION)
-        atomicAnd(reinterpret_cast<unsigned long long*>(t.bits) + (i >> 6), ~(1ull << (i & 63)));
+    const int known = key >= 0 ? (int)((t.committee.flags[key] & KEY_TORSION) != 0) : memo_lookup(t.memo, aw);
+    if (known >= 0) {
+      if (known) atomicAnd(reinterpret_cast<unsigned long long*>(t.bits) + (i >> 6), ~(1ull << (i & 63)));
       continue;
     }
     u32 h = committee_hash(aw[0], aw[1]) & t.slot_mask;
@@ -932,7 +970,9 @@ __global__ __launch_bounds__(256) void k_tors_eval(TorsArgs t) {
     u32 yc[1][8];
     bool ok[1];
     decompress_one(A, aw, yc, ok);
-    t.tflag[h] = (ok[0] && ge_has_torsion(A[0])) ? 1u : 0u;
+    const u32 tor = (ok[0] && ge_has_torsion(A[0])) ? 1u : 0u;
+    t.tflag[h] = tor;
+    if (ok[0]) memo_insert(t.memo, aw, tor);
   }
 }
 __global__ __launch_bounds__(256) void k_tors_apply(TorsArgs t) {
@@ -942,6 +982,13 @@ __global__ __launch_bounds__(256) void k_tors_apply(TorsArgs t) {
     u32 aw[8];
     int key;
     if (!tors_candidate(t, idx, i, aw, key) || key >= 0) continue;
+    // memoised keys (found by k_tors_mark, or memoised by k_tors_eval just now) carry their flag;
+    // clearing a bit k_tors_mark already cleared is harmless
+    const int known = memo_lookup(t.memo, aw);
+    if (known >= 0) {
+      if (known) atomicAnd(reinterpret_cast<unsigned long long*>(t.bits) + (i >> 6), ~(1ull << (i & 63)));
+      continue;
+    }
     // k_tors_mark inserted the key at or before the first empty slot of its probe sequence
     u32 h = committee_hash(aw[0], aw[1]) & t.slot_mask;
     int32_t rep = t.slots[h];

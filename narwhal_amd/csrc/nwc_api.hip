@@ -73,6 +73,8 @@ struct DevCtx {
   uint32_t* ts_uniq = nullptr;
   uint32_t* ts_nuniq = nullptr;
   uint32_t ts_slot_count = 0;
+  nwc::u32* km_keys = nullptr;   // torsion memo of uncached keys (KeyMemo), kept for the context's life
+  nwc::u32* km_flag = nullptr;
   // committee key cache (nwc_set_committee); buffers replaced only after scratch_free
   nwc::u32* cm_keys = nullptr;
   nwc::u32* cm_flags = nullptr;
@@ -111,6 +113,10 @@ struct DevCtx {
   }
 };
 
+// slots of the per-device torsion memo of uncached keys (power of two)
+#ifndef NWC_MEMO_SLOTS
+#define NWC_MEMO_SLOTS (1u << 16)
+#endif
 // committees up to this size get per-key combs (5.8 MB each); larger ones use the cached ladder
 #ifndef NWC_COMB_MAX_KEYS
 #define NWC_COMB_MAX_KEYS 1024
@@ -199,6 +205,10 @@ int init_device(DevCtx& d) {
   hipLaunchKernelGGL(nwc::k_build_base_table16, dim3((2 * nwc::B16_ENTRIES + 255) / 256), dim3(256), 0, d.stream,
                      d.base16);
   HIP_TRY(hipGetLastError());
+  // torsion memo: 64K keys (2.3 MB), all slots empty
+  HIP_TRY(hipMalloc(&d.km_keys, 32 * (size_t)NWC_MEMO_SLOTS));
+  HIP_TRY(hipMalloc(&d.km_flag, 4 * (size_t)NWC_MEMO_SLOTS));
+  HIP_TRY(hipMemsetAsync(d.km_flag, 0xFF, 4 * (size_t)NWC_MEMO_SLOTS, d.stream));
   HIP_TRY(hipStreamSynchronize(d.stream));
   return 0;
 }
@@ -278,7 +288,9 @@ int launch_torsion(DevCtx& d, const uint8_t* pks, uint64_t* out_words, uint64_t 
   if (2 * n > d.ts_slot_count) return set_err(NWC_ERR_ARG, "torsion set too small for %llu equations", (unsigned long long)n);
   HIP_TRY(hipMemsetAsync(d.ts_slots, 0xFF, 4 * (size_t)d.ts_slot_count, s));
   HIP_TRY(hipMemsetAsync(d.ts_nuniq, 0, sizeof(uint32_t), s));
-  const nwc::TorsArgs t{pks, out_words, list, count, n, d.ts_slots, d.ts_slot_count - 1, d.ts_uniq, d.ts_nuniq, d.ts_flag, cm};
+  const nwc::KeyMemo memo{d.km_keys, d.km_flag, NWC_MEMO_SLOTS - 1};
+  const nwc::TorsArgs t{pks, out_words, list, count, n, d.ts_slots, d.ts_slot_count - 1, d.ts_uniq, d.ts_nuniq, d.ts_flag, cm,
+                        memo};
   const uint64_t cap = (uint64_t)d.cus * 8;
   const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, cap);
   hipLaunchKernelGGL(nwc::k_tors_mark, dim3(grid), dim3(256), 0, s, t);
@@ -608,6 +620,8 @@ void nwc_shutdown(void) {
     if (d->ts_flag) (void)hipFree(d->ts_flag);
     if (d->ts_uniq) (void)hipFree(d->ts_uniq);
     if (d->ts_nuniq) (void)hipFree(d->ts_nuniq);
+    if (d->km_keys) (void)hipFree(d->km_keys);
+    if (d->km_flag) (void)hipFree(d->km_flag);
     if (d->scratch_free) (void)hipEventDestroy(d->scratch_free);
     if (d->base_table) (void)hipFree(d->base_table);
     if (d->base16) (void)hipFree(d->base16);

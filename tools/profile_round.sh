@@ -23,4 +23,10 @@ $P --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $R/b
 $P --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py $ARGS > $OUT/pmc_write.log 2>&1
 $P --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT/pmc_clk -o run -- python3 $R/bench.py $ARGS > $OUT/pmc_clk.log 2>&1
 $P --kernel-trace --stats --output-format csv -d $OUT/trace_cfg3 -o run -- python3 $R/bench.py --steps 2 --warmup 1 --cpu-budget 0 --cfg1-calls 0 --triples 65536 --digest-batches 0 --cfg5-total 0 > $OUT/trace_cfg3.log 2>&1
+# instruction-rate microbenchmarks (the VOP3 4-cycle issue rate the roofline quotes beside the
+# guide's 2-cycle peak), built in-tree by `make -C tools/microbench` / hipcc before the call
+mkdir -p $OUT/microbench
+for mb in int_rates sha_ops lattice_cost; do
+  if [ -x $R/tools/microbench/$mb ]; then timeout -k 10 120 $R/tools/microbench/$mb > $OUT/microbench/$mb.txt 2>&1; fi
+done
 echo done
