@@ -108,25 +108,34 @@ __global__ void k_build_base_table(ge_niels* table) {
   table[i] = ge_p3_to_niels(acc);
 }
 
-// Radix-2^16 basepoint tables for the half-size ladder, resident in HBM (8.4 MB; L2/MALL-warm):
-// table16[h * B16_ENTRIES + j] = j * (2^(132 h) B), h = 0, 1, j = 0..32768, affine Niels padded to
-// 128 B (8 x dwordx4, the LDS-DMA granule).  One lane per entry.
-constexpr int B16_ENTRIES = 32769;
+// Radix-2^24 basepoint tables for the half-size ladder, resident in HBM (2.1 GB of the 288):
+// table24[h * B24_ENTRIES + j] = j * (2^(141 h) B), h = 0, 1, j = 0..2^23, affine Niels padded to
+// 128 B (8 x dwordx4, the LDS-DMA granule).  e_B = d s mod l (253 bits) splits at 2^141 into
+// 6 + 5 signed 24-bit digits: 11 Niels adds per equation for the B term (radix 2^16 took 18).
+// Built once per device at init: k_base_pow2 doubles B 141 times on one lane, then one lane
+// per entry runs a 23-bit double-and-add (~30 ms for the 16.8M entries).
+constexpr int B24_SPLIT_BITS = 141;
+constexpr int B24_ENTRIES = (1 << 23) + 1;
 struct ge_niels_pad { ge_niels n; u32 pad[2]; };
 static_assert(sizeof(ge_niels_pad) == 128, "padded Niels entry");
-__global__ void k_build_base_table16(ge_niels_pad* table) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * B16_ENTRIES) return;
+__global__ void k_base_pow2(ge_p3* out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
   ge_p3 b = ge_base_point();
-  if (i >= B16_ENTRIES) {
-    for (int k = 0; k < BASE_SPLIT_BITS; ++k) b = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(b)));
-  }
-  const int j = i % B16_ENTRIES;
-  const ge_cached bc = ge_p3_to_cached(b);
+  out[0] = b;
+  for (int k = 0; k < B24_SPLIT_BITS; ++k) b = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(b)));
+  out[1] = b;
+}
+__global__ void k_build_base_table24(ge_niels_pad* table, const ge_p3* bases) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * (size_t)B24_ENTRIES) return;
+  const int h = i >= (size_t)B24_ENTRIES ? 1 : 0;
+  const u32 j = (u32)(i - (size_t)h * B24_ENTRIES);
+  const ge_cached bc = ge_p3_to_cached(bases[h]);
   ge_p3 acc = ge_p3_identity();
-  for (int bit = 15; bit >= 0; --bit) {
+#pragma unroll 1
+  for (int bit = 23; bit >= 0; --bit) {
     acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
-    if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, bc));
+    if ((j >> bit) & 1u) acc = ge_p1p1_to_p3(ge_add_cached(acc, bc));
   }
   table[i].n = ge_p3_to_niels(acc);
   table[i].pad[0] = 0;
@@ -447,28 +456,42 @@ __device__ __forceinline__ Digits256 recode256(const u32 x[5], int ndig) {
   return r;
 }
 
-// Signed radix-2^16 digits of x < 2^144 (9 digits, d in [-2^15, 2^15)) as 16-bit fields d+2^15,
-// digit 8 in the top half of word 4.  Used for the two 132-bit halves of eB (tables in HBM).
-constexpr int B16_DIGITS = 9;   // windows 32, 28, ..., 0
-struct Digits65536 { u32 w[5]; };
-__device__ __forceinline__ Digits65536 recode65536(const u32 x[5]) {
-  Digits65536 r;
-  _Pragma("unroll") for (int i = 0; i < 5; ++i) r.w[i] = 0;
+// Signed radix-2^24 digits of the two halves of e_B (tables in HBM): lo < 2^141 has 6 digits
+// (windows 30, 24, ..., 0), hi < 2^112 has 5 (windows 24, ..., 0); digits in [-2^23, 2^23) except
+// the top one of each half, which takes the final carry (<= 2^21 + 1 and 2^16 + 1).  A queue of
+// registers, next digit last: consuming one is five moves, no dynamic register indexing.
+constexpr int B24_LO_DIGITS = 6, B24_HI_DIGITS = 5;
+struct Digits24 { i32 d[B24_LO_DIGITS]; };
+template <int N>
+__device__ __forceinline__ Digits24 recode24(const u32 x[5]) {
+  static_assert(N >= 1 && N <= B24_LO_DIGITS, "digit count");
+  constexpr int OFF = B24_LO_DIGITS - N;   // digit i sits at queue slot i + OFF (top digit last)
+  Digits24 r;
+  _Pragma("unroll") for (int i = 0; i < OFF; ++i) r.d[i] = 0;
   i32 carry = 0;
-  _Pragma("unroll") for (int i = 0; i < B16_DIGITS; ++i) {
-    const i32 v = (i32)((x[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) + carry;
-    carry = (v + 32768) >> 16;
-    const i32 d = v - (carry << 16);
-    const int pos = i + 1;
-    r.w[pos >> 1] |= (u32)(d + 32768) << (16 * (pos & 1));
+  _Pragma("unroll") for (int i = 0; i < N; ++i) {
+    const int bit = 24 * i, wi = bit >> 5, sh = bit & 31;
+    u32 v = x[wi] >> sh;
+    if (sh > 8 && wi + 1 < 5) v |= x[wi + 1] << (32 - sh);
+    const i32 t = (i32)(v & 0xFFFFFFu) + carry;
+    if (i == N - 1) {
+      r.d[i + OFF] = t;
+    } else {
+      carry = (t + (1 << 23)) >> 24;
+      r.d[i + OFF] = t - (carry << 24);
+    }
   }
   return r;
 }
-__device__ __forceinline__ i32 next65536(Digits65536& x) {
-  const i32 d = (i32)(x.w[4] >> 16) - 32768;
-  _Pragma("unroll") for (int i = 4; i > 0; --i) x.w[i] = (x.w[i] << 16) | (x.w[i - 1] >> 16);
-  x.w[0] <<= 16;
+__device__ __forceinline__ i32 next24(Digits24& x) {
+  const i32 d = x.d[B24_LO_DIGITS - 1];
+  _Pragma("unroll") for (int i = B24_LO_DIGITS - 1; i > 0; --i) x.d[i] = x.d[i - 1];
+  x.d[0] = 0;
   return d;
+}
+// window w of the half-size ladder consumes 2 (w = 0, 6, .., 24), 1 (w = 30) or 0 basepoint digits
+__device__ __forceinline__ int base_window_digits(int w) {
+  return (w % 6 != 0 || w > 6 * (B24_LO_DIGITS - 1)) ? 0 : (w > 6 * (B24_HI_DIGITS - 1) ? 1 : 2);
 }
 
 // LDS staging of basepoint-table entries fetched by LDS-DMA (global_load_lds_dwordx4): each wave
@@ -521,8 +544,37 @@ __device__ __forceinline__ void ladder_dbl4(ge_p1p1& t) {
   t = ge_p2_dbl(p2);
 }
 
+// Basepoint digits of window w: settle pending loads, then DMA the entries into the wave's stage.
+// Returns the number of entries fetched (0, 1 or 2).
+__device__ __forceinline__ int base_fetch(int w, Digits24& el, Digits24& eh, i32& d0, i32& d1,
+                                          const ge_niels_pad* T24, uint4* stage) {
+  const int nb = base_window_digits(w);
+  if (nb) {
+    d0 = next24(el);
+    // settle the A/R entry loads first (they landed during the doublings), so no wait placed
+    // for them below also has to wait for the DMA
+    stage_wait();
+    stage_fetch(stage, 0, T24 + (d0 < 0 ? -d0 : d0));
+    if (nb == 2) {
+      d1 = next24(eh);
+      stage_fetch(stage, 1, T24 + B24_ENTRIES + (d1 < 0 ? -d1 : d1));
+    }
+  }
+  return nb;
+}
+__device__ __forceinline__ void base_adds(ge_p1p1& t, int nb, i32 d0, i32 d1, const uint4* stage) {
+  if (nb) {
+    stage_wait();
+#pragma unroll 1
+    for (int side = 0; side < nb; ++side) {
+      const i32 dd_ = side ? d1 : d0;
+      t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(stage_read(stage, side), dd_ < 0));
+    }
+  }
+}
+
 __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const LaneTable& tr, Digits16 cd, Digits16 dd,
-                                                 Digits65536 el, Digits65536 eh, const ge_niels_pad* T16,
+                                                 Digits24 el, Digits24 eh, const ge_niels_pad* T24,
                                                  uint4* stage, int W) {
   // Code-size discipline: the window body holds ONE doubling and ONE Niels add (rolled loops) and
   // two cached adds, so the hot loop stays inside the instruction cache.
@@ -534,29 +586,13 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     if (w != W - 1) ladder_dbl4(t);
-    const bool bwin = (w & 3) == 0 && w < 4 * B16_DIGITS;
     i32 d0 = 0, d1 = 0;
-    if (bwin) {
-      d0 = next65536(el);
-      d1 = next65536(eh);
-      // settle the A/R entry loads first (they landed during the doublings), so no wait placed
-      // for them below also has to wait for the DMA
-      stage_wait();
-      stage_fetch(stage, 0, T16 + (d0 < 0 ? -d0 : d0));
-      stage_fetch(stage, 1, T16 + B16_ENTRIES + (d1 < 0 ? -d1 : d1));
-    }
+    const int nb = base_fetch(w, el, eh, d0, d1, T24, stage);
     // two explicit adds (a rolled 2-iteration loop needs a selected copy of the entry: 40 more
     // live VGPRs, which spilled)
     if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(ea, da < 0));
     t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
-    if (bwin) {
-      stage_wait();
-#pragma unroll 1
-      for (int side = 0; side < 2; ++side) {
-        const i32 dd_ = side ? d1 : d0;
-        t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(stage_read(stage, side), dd_ < 0));
-      }
-    }
+    base_adds(t, nb, d0, d1, stage);
     if (w > 0) {
       da = next16(cd);
       dr = next16(dd);
@@ -571,8 +607,8 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
 // radix-256 Niels table (one add at every even window, no per-equation table or decompression).
 // ca: radix-256 digits of |c| starting at window (W-1) & ~1; c_neg flips every A entry.
 __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Digits16 dd, Digits256 ca, bool c_neg,
-                                                        const ge_niels* key_tab, Digits65536 el, Digits65536 eh,
-                                                        const ge_niels_pad* T16, uint4* stage, int W) {
+                                                        const ge_niels* key_tab, Digits24 el, Digits24 eh,
+                                                        const ge_niels_pad* T24, uint4* stage, int W) {
   i32 dr = dd.top;   // >= 0
   ge_cached er = tr.load(dr);
   ge_p1p1 t = ge_cached_to_p1p1(er);
@@ -581,27 +617,11 @@ __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Dig
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     if (w != W - 1) ladder_dbl4(t);
-    const bool bwin = (w & 3) == 0 && w < 4 * B16_DIGITS;
     i32 d0 = 0, d1 = 0;
-    if (bwin) {
-      d0 = next65536(el);
-      d1 = next65536(eh);
-      // settle the A/R entry loads first (they landed during the doublings), so no wait placed
-      // for them below also has to wait for the DMA
-      stage_wait();
-      stage_fetch(stage, 0, T16 + (d0 < 0 ? -d0 : d0));
-      stage_fetch(stage, 1, T16 + B16_ENTRIES + (d1 < 0 ? -d1 : d1));
-    }
+    const int nb = base_fetch(w, el, eh, d0, d1, T24, stage);
     if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
     if ((w & 1) == 0) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(ean, (dA < 0) != c_neg));
-    if (bwin) {
-      stage_wait();
-#pragma unroll 1
-      for (int side = 0; side < 2; ++side) {
-        const i32 dd_ = side ? d1 : d0;
-        t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(stage_read(stage, side), dd_ < 0));
-      }
-    }
+    base_adds(t, nb, d0, d1, stage);
     if (w > 0) {
       dr = next16(dd);
       er = tr.load(dr < 0 ? -dr : dr);
@@ -677,8 +697,8 @@ __device__ bool verify_full(const u32 mw[8], const u32 aw[8], const u32 sigw[16]
   return p.ok && eq;
 }
 
-// e_B = d * s mod l, split at 2^132 into radix-2^16 digit strings (el, eh)
-__device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digits65536& el, Digits65536& eh) {
+// e_B = d * s mod l, split at 2^141 into radix-2^24 digit queues (el, eh)
+__device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digits24& el, Digits24& eh) {
   u32 prod[16];
   _Pragma("unroll") for (int i = 0; i < 16; ++i) prod[i] = 0;
   _Pragma("unroll") for (int x = 0; x < 5; ++x) {
@@ -692,14 +712,14 @@ __device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digi
   }
   u32 eb[8];
   sc_reduce512(prod, eb);
-  constexpr int SH = BASE_SPLIT_BITS - 128;
+  constexpr int SH = B24_SPLIT_BITS - 128;
   u32 lo[5], hi[5];
   _Pragma("unroll") for (int i = 0; i < 4; ++i) lo[i] = eb[i];
   lo[4] = eb[4] & ((1u << SH) - 1u);
   _Pragma("unroll") for (int i = 0; i < 4; ++i) hi[i] = (eb[4 + i] >> SH) | (i + 5 < 8 ? eb[5 + i] << (32 - SH) : 0u);
   hi[4] = 0;
-  el = recode65536(lo);
-  eh = recode65536(hi);
+  el = recode24<B24_LO_DIGITS>(lo);
+  eh = recode24<B24_HI_DIGITS>(hi);
 }
 
 // Half-size equation: [d]e = (d s mod l) B - c A - d R == O  (lattice.h).  Sets `fallback`
@@ -707,7 +727,7 @@ __device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digi
 // When every lane of the wave has its key in the committee cache (wave-uniform test), A comes
 // from the cache: no decompression of A, no per-equation A table, 18 Niels adds for the A term.
 template <bool CACHE>
-__device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels_pad* T16,
+__device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels_pad* T24,
                             uint4* stage, const LaneTable& ta, const LaneTable& tr, const Committee& cm,
                             bool& fallback) {
   const int key = CACHE ? committee_lookup(cm, aw) : -1;
@@ -728,12 +748,12 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
     // odd W: the top radix-256 digit of |c| (window W-1) is then < 2^3 + 1, never 128
     const int W = wave_windows(h.ok ? h.bits : 0) | 1;
     fallback = !h.ok;
-    Digits65536 el, eh;
+    Digits24 el, eh;
     base_digits(h.d, sw, el, eh);
     const Digits16 dd = recode16(h.d, W);
     const Digits256 ca = recode256(h.c, ((W - 1) >> 1) + 1);
     build_table(tr, ge_p3_neg(R[0]));
-    const ge_p2 q = half_scalarmult_cached(tr, dd, ca, h.c_neg, cm.tables + (size_t)key * 129, el, eh, T16, stage, W);
+    const ge_p2 q = half_scalarmult_cached(tr, dd, ca, h.c_neg, cm.tables + (size_t)key * 129, el, eh, T24, stage, W);
     const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
     return ok && ident && h.ok;
   }
@@ -742,13 +762,13 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
   const lat::HalfScalars h = lat::reduce(p.kw);
   const int W = wave_windows(h.ok ? h.bits : 0);
   fallback = !h.ok;
-  Digits65536 el, eh;
+  Digits24 el, eh;
   base_digits(h.d, p.sw, el, eh);
   const Digits16 cd = recode16(h.c, W), dd = recode16(h.d, W);
   // -c A = |c| * (c < 0 ? A : -A);  -d R = d * (-R)
   build_table(ta, h.c_neg ? p.A : ge_p3_neg(p.A));
   build_table(tr, ge_p3_neg(p.R));
-  const ge_p2 q = half_scalarmult(ta, tr, cd, dd, el, eh, T16, stage, W);
+  const ge_p2 q = half_scalarmult(ta, tr, cd, dd, el, eh, T24, stage, W);
   const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
   return p.ok && ident && h.ok;
 }
@@ -770,7 +790,7 @@ struct VerifyArgs {
   uint64_t n;
   int strict;
   const ge_niels* base_table;   // 2 x 129 entries (radix 256; full-length ladder)
-  const ge_niels_pad* base16;   // 2 x B16_ENTRIES entries (radix 2^16; half-size ladder)
+  const ge_niels_pad* base24;   // 2 x B24_ENTRIES entries (radix 2^24; half-size ladder)
   uint8_t* scratch;             // 2 * TAB_BYTES_PER_LANE per lane slot
   uint32_t* fb_list;
   uint32_t* fb_count;
@@ -827,7 +847,7 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
     load_inputs(a, active ? i : 0, mw, aw, sgw);
     bool fb = false;
     bool v;
-    if constexpr (HALF) v = verify_half<CACHE>(mw, aw, sgw, a.strict != 0, a.base16, stage, ta, tr, a.committee, fb);
+    if constexpr (HALF) v = verify_half<CACHE>(mw, aw, sgw, a.strict != 0, a.base24, stage, ta, tr, a.committee, fb);
     else v = verify_full(mw, aw, sgw, a.strict != 0, sB, ta);
     if (HALF && a.force_fb_every && (i % a.force_fb_every) == 0) { fb = true; v = false; }
     v = v && active;

@@ -136,6 +136,101 @@ struct HalfScalars {
   int bits;      // max(bit length |c|, bit length d)
 };
 
+// One step of the exact remainder sequence (a partial-quotient step when q is under-estimated).
+NWC_HD void euclid_step(w32 r0[8], w32 r1[8], w32 t0[5], w32 t1[5]) {
+  const w32 q = quot_est(r0, r1);
+  submul8(r0, r1, q);
+  submul5s(t0, t1, q);
+  if (lt8(r0, r1)) {
+    for (int i = 0; i < 8; ++i) { w32 x = r0[i]; r0[i] = r1[i]; r1[i] = x; }
+    for (int i = 0; i < 5; ++i) { w32 x = t0[i]; t0[i] = t1[i]; t1[i] = x; }
+  }
+}
+
+NWC_HD bool below_2_127(const w32 r[8]) { return (r[7] | r[6] | r[5] | r[4]) == 0 && r[3] < 0x80000000u; }
+
+// 52 bits of x starting at bit s, s in [64, 204] (x < 2^256, so only words 2..7 can be the low one)
+NWC_HD w64 bits52(const w32 x[8], int s) {
+  const int wi = s >> 5, sh = s & 31;
+  w32 a = 0, b = 0, c = 0;
+  for (int i = 2; i < 8; ++i) {
+    a = i == wi ? x[i] : a;
+    b = i == wi + 1 ? x[i] : b;
+    c = i == wi + 2 ? x[i] : c;
+  }
+  const w64 lo = ((w64)b << 32) | a;
+  const w64 v = sh ? (lo >> sh) | ((w64)c << (64 - sh)) : lo;
+  return v & ((1ull << 52) - 1);
+}
+
+// (P - Q) or (Q - P) of P = |a| x, Q = |b| y over N words, mod 2^(32N): one row of the cofactor
+// matrix applied to (x, y).  The row's entries have opposite signs (or one is 0), so the
+// combination a x + b y is |a| x - |b| y when b <= 0 and |b| y - |a| x otherwise.
+template <int N>
+NWC_HD void mat_row(const w32 x[N], const w32 y[N], w32 ma, w32 mb, bool b_pos, w32 out[N]) {
+  w64 cp = 0, cq = 0;
+  w32 p[N], q[N];
+  for (int i = 0; i < N; ++i) {
+    const w64 u = (w64)ma * x[i] + cp, v = (w64)mb * y[i] + cq;
+    p[i] = (w32)u; cp = u >> 32;
+    q[i] = (w32)v; cq = v >> 32;
+  }
+  w64 br = 0;
+  for (int i = 0; i < N; ++i) {
+    const w32 hi = b_pos ? q[i] : p[i], lo = b_pos ? p[i] : q[i];
+    const w64 d = (w64)hi - lo - br;
+    out[i] = (w32)d;
+    br = (d >> 63) & 1;
+  }
+}
+
+// Lehmer block (Knuth TAOCP 4.5.2, Algorithm L): run Euclid on the 52-bit leading parts of
+// (r0, r1) in double precision (every value an exact integer < 2^53), accept a step only when
+// the quotient is certified for the full numbers (Knuth's two-sided test) and the new r1 is
+// certainly still >= 2^127 (so the caller's stopping point, the first r1 < 2^127, is never
+// skipped), then apply the 2x2 cofactor matrix to (r0, r1) and (t0, t1) once.  The remainder
+// sequence stays exactly Euclid's, so (c, d) are bit-identical to reduce<false>.  Returns the
+// number of steps taken (0: the caller takes one exact single-precision step).
+constexpr int MAX_INNER = 48;    // cofactors < 2^31 bound a block to ~45 steps
+constexpr int MAX_OUTER = 96;
+NWC_HD int lehmer_block(w32 r0[8], w32 r1[8], w32 t0[5], w32 t1[5]) {
+  const int s = bitlen8(r0) - 52;   // r0 > r1 >= 2^127: s >= 76
+  double u = (double)bits52(r0, s), v = (double)bits52(r1, s);
+  double A = 1, B = 0, C = 0, D = 1;
+  // the true new r1 lies above (v' + min(C', D')) 2^s: accept while that is >= 2^127
+  const double thr = s >= 127 ? 1.0 : __builtin_ldexp(1.0, 127 - s);
+  constexpr double COF_MAX = 2147483648.0;   // 2^31: the matrix entries fit a u32 magnitude
+  int steps = 0;
+  for (int j = 0; j < MAX_INNER; ++j) {
+    const double d1 = v + C, d2 = v + D;
+    if (!(d1 > 0 && d2 > 0)) break;
+    const double n1 = u + A, n2 = u + B;
+    double q = __builtin_floor(n1 * rcp_nr(d1));
+    double rem = __builtin_fma(-q, d1, n1);   // exact: a small integer
+    if (rem < 0) { q -= 1; rem += d1; }
+    if (rem >= d1) q += 1;
+    const double rem2 = __builtin_fma(-q, d2, n2);
+    if (!(rem2 >= 0 && rem2 < d2)) break;   // quotient not certified
+    const double C2 = __builtin_fma(-q, C, A), D2 = __builtin_fma(-q, D, B), v2 = __builtin_fma(-q, v, u);
+    if (!(__builtin_fabs(C2) < COF_MAX && __builtin_fabs(D2) < COF_MAX)) break;
+    if (!(v2 + __builtin_fmin(C2, D2) >= thr)) break;
+    A = C; B = D; C = C2; D = D2; u = v; v = v2;
+    ++steps;
+  }
+  const bool b_pos = B > 0, d_pos = D > 0;
+  const w32 ma = (w32)__builtin_fabs(A), mb = (w32)__builtin_fabs(B), mc = (w32)__builtin_fabs(C),
+            md = (w32)__builtin_fabs(D);
+  w32 n0[8], n1[8], s0[5], s1[5];
+  mat_row<8>(r0, r1, ma, mb, b_pos, n0);
+  mat_row<8>(r0, r1, mc, md, d_pos, n1);
+  mat_row<5>(t0, t1, ma, mb, b_pos, s0);
+  mat_row<5>(t0, t1, mc, md, d_pos, s1);
+  for (int i = 0; i < 8; ++i) { r0[i] = n0[i]; r1[i] = n1[i]; }
+  for (int i = 0; i < 5; ++i) { t0[i] = s0[i]; t1[i] = s1[i]; }
+  return steps;
+}
+
+template <bool LEHMER = true>
 NWC_HD HalfScalars reduce(const w32 k[8]) {
   w32 r0[8], r1[8], t0[5], t1[5];
   eight_l(r0);
@@ -143,16 +238,17 @@ NWC_HD HalfScalars reduce(const w32 k[8]) {
   for (int i = 0; i < 5; ++i) { t0[i] = 0; t1[i] = 0; }
   t1[0] = 1;
   bool done = false;
-  for (int it = 0; it < MAX_ITERS; ++it) {
-    // stop at the first r1 < 2^127
-    done = (r1[7] | r1[6] | r1[5] | r1[4]) == 0 && r1[3] < 0x80000000u;
-    if (done) break;
-    const w32 q = quot_est(r0, r1);
-    submul8(r0, r1, q);
-    submul5s(t0, t1, q);
-    if (lt8(r0, r1)) {
-      for (int i = 0; i < 8; ++i) { w32 x = r0[i]; r0[i] = r1[i]; r1[i] = x; }
-      for (int i = 0; i < 5; ++i) { w32 x = t0[i]; t0[i] = t1[i]; t1[i] = x; }
+  if (LEHMER) {
+    for (int it = 0; it < MAX_OUTER; ++it) {
+      done = below_2_127(r1);
+      if (done) break;
+      if (lehmer_block(r0, r1, t0, t1) == 0) euclid_step(r0, r1, t0, t1);
+    }
+  } else {
+    for (int it = 0; it < MAX_ITERS; ++it) {
+      done = below_2_127(r1);
+      if (done) break;
+      euclid_step(r0, r1, t0, t1);
     }
   }
   HalfScalars h;

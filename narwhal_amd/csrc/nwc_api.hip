@@ -53,7 +53,8 @@ struct DevCtx {
   int verify_blocks_per_cu = 1;
   hipStream_t stream = nullptr;
   nwc::ge_niels* base_table = nullptr;
-  nwc::ge_niels_pad* base16 = nullptr;   // radix-2^16 basepoint tables (8.4 MB)
+  nwc::ge_niels_pad* base24 = nullptr;   // radix-2^24 basepoint tables (2.1 GB)
+  nwc::ge_p3* base24_points = nullptr;    // B and 2^141 B
   nwc::ge_niels_pad* comb_base = nullptr;   // radix-256 basepoint comb (528 KB): latency kernel
   nwc::ge_niels_pad* comb16 = nullptr;      // radix-2^16 basepoint comb (67 MB): k_verify_comb
   int comb_blocks_per_cu = 1;
@@ -201,9 +202,12 @@ int init_device(DevCtx& d) {
   HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
   hipLaunchKernelGGL(nwc::k_build_base_table, dim3(5), dim3(64), 0, d.stream, d.base_table);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMalloc(&d.base16, 2 * (size_t)nwc::B16_ENTRIES * sizeof(nwc::ge_niels_pad)));
-  hipLaunchKernelGGL(nwc::k_build_base_table16, dim3((2 * nwc::B16_ENTRIES + 255) / 256), dim3(256), 0, d.stream,
-                     d.base16);
+  HIP_TRY(hipMalloc(&d.base24, 2 * (size_t)nwc::B24_ENTRIES * sizeof(nwc::ge_niels_pad)));
+  HIP_TRY(hipMalloc(&d.base24_points, 2 * sizeof(nwc::ge_p3)));
+  hipLaunchKernelGGL(nwc::k_base_pow2, dim3(1), dim3(64), 0, d.stream, d.base24_points);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_build_base_table24, dim3((unsigned)((2 * (size_t)nwc::B24_ENTRIES + 255) / 256)), dim3(256), 0,
+                     d.stream, d.base24, (const nwc::ge_p3*)d.base24_points);
   HIP_TRY(hipGetLastError());
   // torsion memo: 64K keys (2.3 MB), all slots empty
   HIP_TRY(hipMalloc(&d.km_keys, 32 * (size_t)NWC_MEMO_SLOTS));
@@ -318,7 +322,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     // devices'); should a key still be missing on the device, the kernel sets the word after the
     // verdict words instead of listing it, and the caller re-runs the general path.
     const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
-    const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base16,
+    const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24,
                             d.scratch, d.fb_list, d.fb_count, 0u, cm};
     const nwc::CombArgs ca{nullptr, reinterpret_cast<uint32_t*>(out_words + (n + 63) / 64), d.comb_base, d.comb16};
     if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64 + 1), s));
@@ -347,7 +351,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
   }();
   const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
-  nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base16, d.scratch,
+  nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
   const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
   const bool half = path != VPath::Full;
@@ -624,7 +628,8 @@ void nwc_shutdown(void) {
     if (d->km_flag) (void)hipFree(d->km_flag);
     if (d->scratch_free) (void)hipEventDestroy(d->scratch_free);
     if (d->base_table) (void)hipFree(d->base_table);
-    if (d->base16) (void)hipFree(d->base16);
+    if (d->base24) (void)hipFree(d->base24);
+    if (d->base24_points) (void)hipFree(d->base24_points);
     if (d->stream) (void)hipStreamDestroy(d->stream);
   }
   g_devs.clear();

@@ -27,12 +27,12 @@ def lat():
     return lib
 
 
-def run(lib, k):
+def run(lib, k, fn="lat_reduce"):
     kw = (ctypes.c_uint32 * 8)(*[(k >> (32 * i)) & 0xFFFFFFFF for i in range(8)])
     c = (ctypes.c_uint32 * 5)()
     d = (ctypes.c_uint32 * 5)()
     cn, ok = ctypes.c_int(), ctypes.c_int()
-    lib.lat_reduce(kw, c, d, ctypes.byref(cn), ctypes.byref(ok))
+    getattr(lib, fn)(kw, c, d, ctypes.byref(cn), ctypes.byref(ok))
     cv = sum(c[i] << (32 * i) for i in range(5))
     dv = sum(d[i] << (32 * i) for i in range(5))
     return (-cv if cn.value else cv), dv, bool(ok.value)
@@ -81,3 +81,18 @@ def test_adversarial_structure(lat):
         c, d, ok = run(lat, k)
         if ok:
             check(k, c, d, ok)
+
+
+def test_lehmer_equals_single_steps(lat):
+    """The Lehmer blocks certify every quotient and never step past the first r1 < 2^127, so
+    the kernels' reduction returns exactly what one-step-at-a-time Euclid returns."""
+    rng = random.Random(11)
+    ks = [rng.randrange(L) for _ in range(20000)]
+    ks += [(N * rng.randrange(1, 2**20) // rng.randrange(1, 2**20) + rng.randrange(-2**40, 2**40)) % L
+           for _ in range(3000)]
+    ks += [0, 1, 2**127 - 1, 2**127, 2**127 + 1, L - 1, L // 2, L // 3, 2**252]
+    for k in ks:
+        a, b = run(lat, k), run(lat, k, "lat_reduce_single")
+        assert a[2] == b[2], k
+        if a[2]:   # failed lanes (e.g. k = 2^252) go to the full-length ladder either way
+            assert a == b, k

@@ -7,13 +7,14 @@
 #include "sha512.h"
 using namespace nwc;
 
+template <bool LEHMER>
 __global__ __launch_bounds__(256, 2) void k_lat(const uint32_t* ks, uint32_t* out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k[8];
   for (int j = 0; j < 8; ++j) k[j] = ks[8 * i + j];
   k[7] &= 0x0FFFFFFFu;
-  lat::HalfScalars h = lat::reduce(k);
+  lat::HalfScalars h = lat::reduce<LEHMER>(k);
   out[i] = h.c[0] ^ h.d[1] ^ (h.ok ? 1u : 0u) ^ (uint32_t)h.bits;
 }
 __global__ __launch_bounds__(256, 2) void k_sha(const uint32_t* ks, uint32_t* out, int n) {
@@ -37,16 +38,17 @@ int main() {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  for (int kind = 0; kind < 2; ++kind) {
+  for (int kind = 0; kind < 3; ++kind) {
     for (int rep = 0; rep < 3; ++rep) {
       hipEventRecord(a);
-      if (kind == 0) k_lat<<<n / 256, 256>>>(dk, dout, n);
+      if (kind == 0) k_lat<true><<<n / 256, 256>>>(dk, dout, n);
+      else if (kind == 1) k_lat<false><<<n / 256, 256>>>(dk, dout, n);
       else k_sha<<<n / 256, 256>>>(dk, dout, n);
       hipEventRecord(b);
       hipEventSynchronize(b);
       float ms;
       hipEventElapsedTime(&ms, a, b);
-      if (rep == 2) printf("%s: %.3f ms per 1M lanes\n", kind ? "sha512 block" : "lat::reduce", ms);
+      if (rep == 2) printf("%s: %.3f ms per 1M lanes\n", kind == 2 ? "sha512 block" : kind == 1 ? "lat::reduce<single steps>" : "lat::reduce<Lehmer>", ms);
     }
   }
   return 0;
