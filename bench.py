@@ -177,40 +177,51 @@ def cfg4_host_batch(b: int) -> bytes:
 
 
 def bench_cfg1(lib, calls: int = 10000, cpu_baseline: bool = False):
-    """BASELINE config 1: Signature::verify_batch on a 4-node certificate (3 votes, 32-byte
-    digest) through the host ABI (H2D + kernel + D2H per call).  Latency-bound by design.
-    Timed without and with the committee cache (the 4 authorities' keys, as a node always has
-    its committee: config/src/lib.rs Committee); the cached leg runs the latency kernel."""
-    from narwhal_amd import _lib, device
-    import torch
-    n = 3
-    seeds = device.derive32(b"nw-cfg1-key", 0, n + 1)
-    digest = device.derive32(b"nw-cfg1-digest", 0, 1)
-    allpk, _ = device.keygen_sign(seeds, digest.repeat(n + 1, 1))
-    pks, sigs = device.keygen_sign(seeds[:n].contiguous(), digest.repeat(n, 1))
-    torch.cuda.synchronize()
-    d, p, s = (t.cpu().numpy().tobytes() for t in (digest, pks, sigs))
-    committee = allpk.cpu().numpy()
-    out = {"workload": "cfg1: verify_batch, 3 votes of a 4-node committee, host ABI incl. H2D/D2H"}
-    for tag, cache in (("no_cache", False), ("cache", True)):
-        if cache:
-            _lib.check(lib.nwc_set_committee(_lib.buf(committee), n + 1))
+    """BASELINE config 1 (SURVEY.md §8(d)): Signature::verify_batch on the reference's 4-node
+    certificate -- the crypto_tests.rs fixture keys (ChaCha20-seeded, tests/golden), digest =
+    SHA-512("Hello, world!")[..32], votes of keys 3, 2, 1 (crypto_tests.rs:79-94) -- through the
+    host ABI (H2D + kernel + D2H per call).  Latency-bound by design.  Timed without and with the
+    committee cache (the 4 authorities' keys, as a node always has its committee:
+    config/src/lib.rs Committee); the cached leg runs the latency kernel, and also times the
+    reference's invalid variant (key 1's signature replaced by 64 zero bytes, :96-115)."""
+    from narwhal_amd import _lib
+    gv = json.load(open(os.path.join(ROOT, "tests", "golden", "ed25519_verify.json")))
+    gb = {c["name"]: c for c in json.load(open(os.path.join(ROOT, "tests", "golden", "ed25519_batch.json")))}
+    committee = np.stack([np.frombuffer(bytes.fromhex(x), np.uint8) for x in gv["reference_keys"]["pks"]])
+
+    def case(name):
+        c = gb[name]
+        d = bytes.fromhex(c["msg"])
+        p = b"".join(bytes.fromhex(v[0]) for v in c["votes"])
+        s = b"".join(bytes.fromhex(v[1]) for v in c["votes"])
+        return d, p, s, len(c["votes"]), 0 if c["verdict"] is True else 1
+
+    d, p, s, n, want = case("ref-verify_valid_batch")
+    assert d.hex() == gv["hello_digest"] and n == 3 and want == 0
+    out = {"workload": "cfg1: verify_batch, the reference's 3-vote certificate of its 4-node committee "
+                       "(crypto_tests.rs:79-94), host ABI incl. H2D/D2H"}
+
+    def timed(d, p, s, n, want):
         lat = []
         first_us = None
         for i in range(calls + 50):
             t0 = time.perf_counter()
             rc = lib.nwc_verify_batch(_lib.buf(d), _lib.buf(p), _lib.buf(s), n, None)
             dt = time.perf_counter() - t0
-            assert rc == 0, rc
+            assert rc == want, (rc, want)
             if i == 0:
                 first_us = dt * 1e6   # uncached keys: includes their torsion test (then memoised)
             if i >= 50:
                 lat.append(dt)
-        if cache:
-            _lib.check(lib.nwc_set_committee(None, 0))
         lat = np.array(lat) * 1e6
-        out[tag] = {"calls": calls, "first_call_us": first_us, "p50_us": float(np.percentile(lat, 50)),
-                    "p99_us": float(np.percentile(lat, 99)), "calls_per_s": float(1e6 / lat.mean())}
+        return {"calls": calls, "first_call_us": first_us, "p50_us": float(np.percentile(lat, 50)),
+                "p99_us": float(np.percentile(lat, 99)), "calls_per_s": float(1e6 / lat.mean())}
+
+    out["no_cache"] = timed(d, p, s, n, want)
+    _lib.check(lib.nwc_set_committee(_lib.buf(committee), len(committee)))
+    out["cache"] = timed(d, p, s, n, want)
+    out["cache_invalid_variant"] = timed(*case("ref-verify_invalid_batch"))
+    _lib.check(lib.nwc_set_committee(None, 0))
     if cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_cfg1(d, p, s, n, min(calls, 2000))
     return out
