@@ -73,6 +73,13 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
  * depend on it. */
 int nwc_set_committee(const uint8_t* pks, size_t n);
 
+/* Key caches of the calling thread's device (nwc_dev_set_device): keys in the committee cache,
+ * and in the auto key cache -- keys of small host calls (<= 1024 equations) outside the
+ * committee cache, added the second time they are seen, so that a node's repeated certificates
+ * take the latency kernel without nwc_set_committee (NWC_AUTO_KEYS = capacity, 0 = off).
+ * Diagnostics only: verdicts never depend on either cache.  Not part of the crate's API. */
+int nwc_cache_stats(uint32_t* committee_keys, uint32_t* auto_keys);
+
 /* ---- primary messages ---------------------------------------- */
 /* config::Committee for the message checks (config/src/lib.rs:134-212): n authorities with
  * their keys, stakes (Committee::stake) and worker ids (Committee::worker): authority k runs

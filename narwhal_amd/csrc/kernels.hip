@@ -501,7 +501,12 @@ __device__ __forceinline__ int base_window_digits(int w) {
 // latency hides behind ~2.6k VALU instructions and no VGPR holds the entry meanwhile.
 typedef __attribute__((address_space(1))) void nwc_gvoid;
 typedef __attribute__((address_space(3))) void nwc_lvoid;
-constexpr int STAGE_U4_PER_WAVE = 16 * 64;
+// NWC_STAGE_ENTRIES = 1 halves the stage (8 KB per wave) for occupancies above 2 waves per SIMD:
+// the second entry of a window is then fetched after the first one has been read.
+#ifndef NWC_STAGE_ENTRIES
+#define NWC_STAGE_ENTRIES 2
+#endif
+constexpr int STAGE_U4_PER_WAVE = NWC_STAGE_ENTRIES * 8 * 64;
 __device__ __forceinline__ void stage_fetch(uint4* stage, int e, const ge_niels_pad* src) {
   const uint4* g = reinterpret_cast<const uint4*>(src);
   _Pragma("unroll") for (int c = 0; c < 8; ++c)
@@ -557,18 +562,25 @@ __device__ __forceinline__ int base_fetch(int w, Digits24& el, Digits24& eh, i32
     stage_fetch(stage, 0, T24 + (d0 < 0 ? -d0 : d0));
     if (nb == 2) {
       d1 = next24(eh);
-      stage_fetch(stage, 1, T24 + B24_ENTRIES + (d1 < 0 ? -d1 : d1));
+      if (NWC_STAGE_ENTRIES == 2) stage_fetch(stage, 1, T24 + B24_ENTRIES + (d1 < 0 ? -d1 : d1));
     }
   }
   return nb;
 }
-__device__ __forceinline__ void base_adds(ge_p1p1& t, int nb, i32 d0, i32 d1, const uint4* stage) {
+__device__ __forceinline__ void base_adds(ge_p1p1& t, int nb, i32 d0, i32 d1, uint4* stage,
+                                          const ge_niels_pad* T24) {
   if (nb) {
     stage_wait();
 #pragma unroll 1
     for (int side = 0; side < nb; ++side) {
       const i32 dd_ = side ? d1 : d0;
-      t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(stage_read(stage, side), dd_ < 0));
+      const ge_niels e = stage_read(stage, NWC_STAGE_ENTRIES == 2 ? side : 0);
+      if (NWC_STAGE_ENTRIES == 1 && side + 1 < nb) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): entry 0 is in VGPRs before the slot is reused
+        stage_fetch(stage, 0, T24 + B24_ENTRIES + (d1 < 0 ? -d1 : d1));
+      }
+      t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(e, dd_ < 0));
+      if (NWC_STAGE_ENTRIES == 1 && side + 1 < nb) stage_wait();
     }
   }
 }
@@ -592,7 +604,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
     // live VGPRs, which spilled)
     if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(ea, da < 0));
     t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
-    base_adds(t, nb, d0, d1, stage);
+    base_adds(t, nb, d0, d1, stage, T24);
     if (w > 0) {
       da = next16(cd);
       dr = next16(dd);
@@ -621,7 +633,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Dig
     const int nb = base_fetch(w, el, eh, d0, d1, T24, stage);
     if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
     if ((w & 1) == 0) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(ean, (dA < 0) != c_neg));
-    base_adds(t, nb, d0, d1, stage);
+    base_adds(t, nb, d0, d1, stage, T24);
     if (w > 0) {
       dr = next16(dd);
       er = tr.load(dr < 0 ? -dr : dr);
@@ -638,9 +650,16 @@ __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Dig
 // points of an equation are decoded one after the other; each field op inside is already 10
 // independent multiply-accumulate chains (fe_asm.h), and interleaving two exponentiations
 // doubled the live field elements past the 2-waves/SIMD register budget.
-__device__ __noinline__ void decompress_one(ge_p3 out[1], const u32* a, u32 ycanon[1][8], bool ok[1]) {
+// K separates the copy called by the half-size k_verify kernels (K = 1) from the others, so the
+// register budget of their launch bounds reaches it (a callee shared with lower-occupancy
+// kernels would be allocated for the most permissive caller).
+template <int K>
+__device__ __noinline__ void decompress_k(ge_p3 out[1], const u32* a, u32 ycanon[1][8], bool ok[1]) {
   const u32* const w[1] = {a};
   ge_decompressN<1>(out, w, ycanon, ok);
+}
+__device__ __forceinline__ void decompress_one(ge_p3 out[1], const u32* a, u32 ycanon[1][8], bool ok[1]) {
+  decompress_k<0>(out, a, ycanon, ok);
 }
 
 // k = SHA-512(R || A || M) mod l over the raw input bytes (one block: 96 bytes + padding)
@@ -669,6 +688,7 @@ struct Prologue {
   u32 kw[8], sw[8];
   bool ok;   // s < l, A and R decode, and (strict) neither is small-order
 };
+template <int K = 0>
 __device__ __forceinline__ void prologue(Prologue& p, const u32 mw[8], const u32 aw[8], const u32 sigw[16],
                                          bool strict) {
   u32 rw[8];
@@ -676,8 +696,8 @@ __device__ __forceinline__ void prologue(Prologue& p, const u32 mw[8], const u32
   const bool s_ok = sc_lt_l(p.sw);
   u32 ya[1][8], yr[1][8];
   bool oka[1], okr[1];
-  decompress_one(&p.A, aw, ya, oka);
-  decompress_one(&p.R, rw, yr, okr);
+  decompress_k<K>(&p.A, aw, ya, oka);
+  decompress_k<K>(&p.R, rw, yr, okr);
   const bool small = strict && (ycanon_is_small_order(ya[0]) || ycanon_is_small_order(yr[0]));
   p.ok = s_ok && oka[0] && okr[0] && !small;
   challenge(rw, aw, mw, p.kw);
@@ -738,7 +758,7 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
     ge_p3 R[1];
     u32 yr[1][8];
     bool r_ok[1];
-    decompress_one(R, rw, yr, r_ok);
+    decompress_k<1>(R, rw, yr, r_ok);
     const u32 fl = cm.flags[key];
     const bool small = strict && ycanon_is_small_order(yr[0]);
     const bool ok = s_ok && key_flags_ok(fl, strict) && r_ok[0] && !small;
@@ -758,7 +778,7 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
     return ok && ident && h.ok;
   }
   Prologue p;
-  prologue(p, mw, aw, sigw, strict);
+  prologue<1>(p, mw, aw, sigw, strict);
   const lat::HalfScalars h = lat::reduce(p.kw);
   const int W = wave_windows(h.ok ? h.bits : 0);
   fallback = !h.ok;

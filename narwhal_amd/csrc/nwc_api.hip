@@ -47,6 +47,55 @@ int set_err(int code, const char* fmt, ...) {
                      __FILE__, __LINE__);                                                       \
   } while (0)
 
+// Exact 32-byte key lookup with the device's hash and probing (committee_lookup): the host copy
+// of a device key cache, so that small host calls can tell before launching whether every key
+// is cached.
+struct KeyIndex {
+  std::vector<nwc::u32> keys;   // 8 words per key
+  std::vector<int32_t> slots;   // slot -> key index, -1 empty
+  uint32_t mask = 0;
+  bool find(const uint8_t* pk) const {
+    if (slots.empty()) return false;
+    nwc::u32 w[8];
+    std::memcpy(w, pk, 32);
+    const nwc::u32 h = nwc::committee_hash(w[0], w[1]);
+    for (int p = 0; p < nwc::COMMITTEE_MAX_PROBE; ++p) {
+      const int32_t idx = slots[(h + p) & mask];
+      if (idx < 0) return false;
+      if (std::memcmp(&keys[8 * (size_t)idx], w, 32) == 0) return true;
+    }
+    return false;
+  }
+  bool all_found(const uint8_t* pks, uint64_t n) const {
+    for (uint64_t i = 0; i < n; ++i)
+      if (!find(pks + 32 * i)) return false;
+    return true;
+  }
+};
+
+// Open-addressing slot table over the first n keys (load factor <= 1/4, probe length bounded by
+// COMMITTEE_MAX_PROBE; a duplicate key keeps its first index).
+uint32_t build_slots(const std::vector<nwc::u32>& keys, size_t n, std::vector<int32_t>& table) {
+  uint32_t slots = 16;
+  while (slots < 4 * n) slots <<= 1;
+  for (;;) {
+    table.assign(slots, -1);
+    bool fits = true;
+    for (size_t i = 0; i < n && fits; ++i) {
+      const nwc::u32 h = nwc::committee_hash(keys[8 * i], keys[8 * i + 1]);
+      int p = 0;
+      for (; p < nwc::COMMITTEE_MAX_PROBE; ++p) {
+        int32_t& slot = table[(h + p) & (slots - 1)];
+        if (slot < 0) { slot = (int32_t)i; break; }
+        if (std::memcmp(&keys[8 * slot], &keys[8 * i], 32) == 0) break;   // duplicate key
+      }
+      fits = p < nwc::COMMITTEE_MAX_PROBE;
+    }
+    if (fits) return slots;
+    slots <<= 1;
+  }
+}
+
 struct DevCtx {
   int hip_id = 0;
   int cus = 0;
@@ -95,6 +144,17 @@ struct DevCtx {
   size_t msg_arena_cap = 0;
   uint8_t* pinned = nullptr;   // host staging for small calls: one H2D and one D2H per call
   size_t pinned_cap = 0;
+  // auto key cache (NWC_AUTO_KEYS): keys of small host calls outside the committee cache, added
+  // with their flags, 129-entry tables and combs the second time they are seen, so that repeated
+  // first-sight certificates take the latency kernel; append-only, guarded by mu like the rest
+  nwc::u32* ak_keys = nullptr;
+  nwc::u32* ak_flags = nullptr;
+  nwc::ge_niels* ak_tables = nullptr;
+  nwc::ge_niels_pad* ak_comb = nullptr;
+  int32_t* ak_slots = nullptr;
+  uint32_t ak_n = 0, ak_cap = 0, ak_slot_cap = 0;
+  KeyIndex ak_host;                       // host copy of the auto cache's lookup table
+  std::vector<nwc::u32> ak_seen;          // keys seen once (8 words each), bounded
   std::mutex mu;
 
   int ensure_pinned(size_t bytes) {
@@ -138,29 +198,12 @@ struct DevCtx {
 std::mutex g_mu;
 std::vector<std::unique_ptr<DevCtx>> g_devs;
 
-// Host copy of the committee key cache's lookup table (same hash and probing as the device), so
-// that small host calls can tell before launching whether every key is cached.
 struct HostCommittee {
   std::mutex mu;
-  std::vector<nwc::u32> keys;
-  std::vector<int32_t> slots;
-  uint32_t mask = 0;
+  KeyIndex idx;
   bool all_cached(const uint8_t* pks, uint64_t n) {
     std::lock_guard<std::mutex> lk(mu);
-    if (slots.empty()) return false;
-    for (uint64_t i = 0; i < n; ++i) {
-      nwc::u32 w[8];
-      std::memcpy(w, pks + 32 * i, 32);
-      const nwc::u32 h = nwc::committee_hash(w[0], w[1]);
-      bool found = false;
-      for (int p = 0; p < nwc::COMMITTEE_MAX_PROBE && !found; ++p) {
-        const int32_t idx = slots[(h + p) & mask];
-        if (idx < 0) break;
-        found = std::memcmp(&keys[8 * (size_t)idx], w, 32) == 0;
-      }
-      if (!found) return false;
-    }
-    return true;
+    return idx.all_found(pks, n);
   }
 };
 HostCommittee g_hcm;
@@ -224,6 +267,98 @@ DevCtx* ctx(int i) {
 
 int require_init() {
   if (g_devs.empty()) return set_err(NWC_ERR_NOT_INIT, "nwc_init has not been called (or found no device)");
+  return 0;
+}
+
+// NWC_AUTO_KEYS: capacity of the per-device auto key cache (default 256 keys, 5.8 MB of combs
+// each, allocated on first use; 0 disables it).
+uint32_t auto_keys_cap() {
+  static const uint32_t cap = [] {
+    const char* e = std::getenv("NWC_AUTO_KEYS");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 256u;
+  }();
+  return cap;
+}
+constexpr size_t AUTO_SEEN_MAX = 4096;   // keys remembered as seen once (cleared when full)
+
+// Keys of a small host call that missed every cache: a key seen before is added to the auto
+// cache (flags, 129-entry table and comb built on d.stream after this call's work; the next call
+// on this device is ordered after the build), a new one is remembered as seen.  The host copy
+// is updated only after the build is enqueued.  Caller holds d.mu and has set the device.
+int auto_insert(DevCtx& d, const uint8_t* pks, uint64_t n) {
+  const uint32_t cap = auto_keys_cap();
+  if (cap == 0 || d.ak_n >= cap) return 0;
+  std::vector<nwc::u32> add;
+  for (uint64_t i = 0; i < n && d.ak_n + add.size() / 8 < cap; ++i) {
+    const uint8_t* k = pks + 32 * i;
+    if (d.ak_host.find(k)) continue;
+    bool dup = false;
+    for (size_t j = 0; j < add.size() && !dup; j += 8) dup = std::memcmp(&add[j], k, 32) == 0;
+    if (dup) continue;
+    bool seen = false;
+    for (size_t j = 0; j < d.ak_seen.size() && !seen; j += 8) seen = std::memcmp(&d.ak_seen[j], k, 32) == 0;
+    if (!seen) {
+      if (d.ak_seen.size() >= 8 * AUTO_SEEN_MAX) d.ak_seen.clear();
+      d.ak_seen.insert(d.ak_seen.end(), reinterpret_cast<const nwc::u32*>(k), reinterpret_cast<const nwc::u32*>(k) + 8);
+      continue;
+    }
+    add.insert(add.end(), reinterpret_cast<const nwc::u32*>(k), reinterpret_cast<const nwc::u32*>(k) + 8);
+  }
+  const uint32_t m = (uint32_t)(add.size() / 8);
+  if (m == 0) return 0;
+  const uint32_t n0 = d.ak_n, n1 = n0 + m;
+  if (n1 > d.ak_cap) {
+    // grow (doubling, at most the configured capacity): copy what is built, free the old arrays
+    // once the stream has drained
+    const uint32_t ncap = std::min(cap, std::max<uint32_t>(16u, 2 * n1));
+    nwc::u32 *keys = nullptr, *flags = nullptr;
+    nwc::ge_niels* tables = nullptr;
+    nwc::ge_niels_pad* comb = nullptr;
+    HIP_TRY(hipMalloc(&keys, 32 * (size_t)ncap));
+    HIP_TRY(hipMalloc(&flags, 4 * (size_t)ncap));
+    HIP_TRY(hipMalloc(&tables, (size_t)ncap * 129 * sizeof(nwc::ge_niels)));
+    HIP_TRY(hipMalloc(&comb, (size_t)ncap * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad)));
+    if (n0) {
+      HIP_TRY(hipMemcpyAsync(keys, d.ak_keys, 32 * (size_t)n0, hipMemcpyDeviceToDevice, d.stream));
+      HIP_TRY(hipMemcpyAsync(flags, d.ak_flags, 4 * (size_t)n0, hipMemcpyDeviceToDevice, d.stream));
+      HIP_TRY(hipMemcpyAsync(tables, d.ak_tables, (size_t)n0 * 129 * sizeof(nwc::ge_niels), hipMemcpyDeviceToDevice, d.stream));
+      HIP_TRY(hipMemcpyAsync(comb, d.ak_comb, (size_t)n0 * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad),
+                             hipMemcpyDeviceToDevice, d.stream));
+    }
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    if (d.ak_keys) HIP_TRY(hipFree(d.ak_keys));
+    if (d.ak_flags) HIP_TRY(hipFree(d.ak_flags));
+    if (d.ak_tables) HIP_TRY(hipFree(d.ak_tables));
+    if (d.ak_comb) HIP_TRY(hipFree(d.ak_comb));
+    d.ak_keys = keys; d.ak_flags = flags; d.ak_tables = tables; d.ak_comb = comb;
+    d.ak_cap = ncap;
+  }
+  KeyIndex next = d.ak_host;
+  next.keys.insert(next.keys.end(), add.begin(), add.end());
+  std::vector<int32_t> table;
+  const uint32_t slots = build_slots(next.keys, n1, table);
+  if (slots > d.ak_slot_cap) {
+    HIP_TRY(hipStreamSynchronize(d.stream));   // no launch still reads the old slot table
+    if (d.ak_slots) HIP_TRY(hipFree(d.ak_slots));
+    d.ak_slots = nullptr;
+    HIP_TRY(hipMalloc(&d.ak_slots, 4 * (size_t)slots));
+    d.ak_slot_cap = slots;
+  }
+  HIP_TRY(hipMemcpyAsync(d.ak_keys + 8 * (size_t)n0, add.data(), 32 * (size_t)m, hipMemcpyHostToDevice, d.stream));
+  hipLaunchKernelGGL(nwc::k_build_key_tables, dim3((unsigned)((m * 129 + 255) / 256)), dim3(256), 0, d.stream,
+                     d.ak_keys + 8 * (size_t)n0, m, d.ak_tables + (size_t)n0 * 129, d.ak_flags + n0);
+  HIP_TRY(hipGetLastError());
+  const size_t entries = (size_t)m * nwc::COMB_PER_KEY;
+  hipLaunchKernelGGL(nwc::k_build_comb<nwc::KeyComb>, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, d.stream,
+                     d.ak_keys + 8 * (size_t)n0, m, d.ak_comb + (size_t)n0 * nwc::COMB_PER_KEY);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(d.ak_slots, table.data(), 4 * (size_t)slots, hipMemcpyHostToDevice, d.stream));
+  // synchronous: the host vectors above are the copy sources
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  next.slots = std::move(table);
+  next.mask = slots - 1;
+  d.ak_host = std::move(next);
+  d.ak_n = n1;
   return 0;
 }
 
@@ -308,13 +443,24 @@ int launch_torsion(DevCtx& d, const uint8_t* pks, uint64_t* out_words, uint64_t 
 
 // launch_verify flags: the caller checked on the host that every key is in the committee cache,
 // and/or out_words is already zero (both let the latency path run as a single kernel)
-constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2;
+constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4;   // LV_AUTO: the keys are in the auto cache
 
 int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
                   hipStream_t s, int flags = 0) {
   if (n == 0) return 0;
   const VPath path = verify_path();
+  if ((flags & LV_AUTO) && (flags & LV_ALL_CACHED) && path == VPath::Default && n <= NWC_WIDE_MAX && d.ak_n) {
+    // latency path over the auto key cache (same kernel, the auto cache as its committee)
+    const nwc::Committee cm{d.ak_keys, d.ak_flags, d.ak_tables, d.ak_comb, d.ak_slots, d.ak_host.mask, d.ak_n};
+    const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24,
+                            d.scratch, d.fb_list, d.fb_count, 0u, cm};
+    const nwc::CombArgs ca{nullptr, reinterpret_cast<uint32_t*>(out_words + (n + 63) / 64), d.comb_base, d.comb16};
+    if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64 + 1), s));
+    hipLaunchKernelGGL(nwc::k_verify_comb_wide, dim3((unsigned)n), dim3(128), 0, s, a, ca);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   const bool comb = path == VPath::Default && d.cm_n && d.cm_comb;
   if (comb && n <= NWC_WIDE_MAX && (flags & LV_ALL_CACHED)) {
     // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none).
@@ -508,7 +654,9 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     std::memset(h + ((uint8_t*)dout - d.arena), 0, 8 * (words + 1));
     HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena) + 8 * (words + 1), hipMemcpyHostToDevice,
                            d.stream));
-    const int fl = LV_OUT_ZEROED | (d.cm_n && g_hcm.all_cached(pks + 32 * lo, n) ? LV_ALL_CACHED : 0);
+    int fl = LV_OUT_ZEROED;
+    if (d.cm_n && g_hcm.all_cached(pks + 32 * lo, n)) fl |= LV_ALL_CACHED;
+    else if (d.ak_n && n <= NWC_WIDE_MAX && d.ak_host.all_found(pks + 32 * lo, n)) fl |= LV_ALL_CACHED | LV_AUTO;
     if (int rc = launch_verify(d, dm, dmi, msg_stride ? 1 : 0, dp, ds, n, strict, dout, d.stream, fl)) return rc;
     HIP_TRY(hipMemcpyAsync(h, dout, 8 * (words + 1), hipMemcpyDeviceToHost, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
@@ -519,6 +667,8 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
       HIP_TRY(hipStreamSynchronize(d.stream));
     }
     std::memcpy(out_words.data(), h, 8 * words);
+    if (!(fl & LV_ALL_CACHED) && n <= NWC_WIDE_MAX && verify_path() == VPath::Default)
+      if (int rc = auto_insert(d, pks + 32 * lo, n)) return rc;
     return 0;
   }
   if (msg_index) {
@@ -611,6 +761,11 @@ void nwc_shutdown(void) {
     if (d->cm_tables) (void)hipFree(d->cm_tables);
     if (d->cm_slots) (void)hipFree(d->cm_slots);
     if (d->cm_comb) (void)hipFree(d->cm_comb);
+    if (d->ak_keys) (void)hipFree(d->ak_keys);
+    if (d->ak_flags) (void)hipFree(d->ak_flags);
+    if (d->ak_tables) (void)hipFree(d->ak_tables);
+    if (d->ak_comb) (void)hipFree(d->ak_comb);
+    if (d->ak_slots) (void)hipFree(d->ak_slots);
     if (d->comb_base) (void)hipFree(d->comb_base);
     if (d->comb16) (void)hipFree(d->comb16);
     if (d->pinned) (void)hipHostFree(d->pinned);
@@ -742,30 +897,13 @@ static int set_committee_locked(const uint8_t* pks, size_t n) {
   // open-addressing table (exact 32-byte keys), load factor <= 1/4, probe length bounded
   std::vector<nwc::u32> keys(8 * n);
   std::memcpy(keys.data(), pks, 32 * n);
-  uint32_t slots = 16;
-  while (slots < 4 * n) slots <<= 1;
   std::vector<int32_t> table;
-  for (;;) {
-    table.assign(slots, -1);
-    bool fits = true;
-    for (size_t i = 0; i < n && fits; ++i) {
-      const nwc::u32 h = nwc::committee_hash(keys[8 * i], keys[8 * i + 1]);
-      int p = 0;
-      for (; p < nwc::COMMITTEE_MAX_PROBE; ++p) {
-        int32_t& slot = table[(h + p) & (slots - 1)];
-        if (slot < 0) { slot = (int32_t)i; break; }
-        if (std::memcmp(&keys[8 * slot], &keys[8 * i], 32) == 0) break;   // duplicate key
-      }
-      fits = p < nwc::COMMITTEE_MAX_PROBE;
-    }
-    if (fits) break;
-    slots <<= 1;
-  }
+  const uint32_t slots = build_slots(keys, n, table);
   {
     // host view cleared while the devices change (a call in between takes the general path),
     // set again once every device holds the new cache (end of this function)
     std::lock_guard<std::mutex> lk(g_hcm.mu);
-    g_hcm.slots.clear();
+    g_hcm.idx.slots.clear();
   }
   for (auto& dp : g_devs) {
     DevCtx& d = *dp;
@@ -811,10 +949,19 @@ static int set_committee_locked(const uint8_t* pks, size_t n) {
   }
   if (n) {
     std::lock_guard<std::mutex> lk(g_hcm.mu);
-    g_hcm.keys = keys;
-    g_hcm.slots = table;
-    g_hcm.mask = slots - 1;
+    g_hcm.idx.keys = keys;
+    g_hcm.idx.slots = table;
+    g_hcm.idx.mask = slots - 1;
   }
+  return 0;
+}
+
+int nwc_cache_stats(uint32_t* committee_keys, uint32_t* auto_keys) {
+  if (int rc = require_init()) return rc;
+  DevCtx& d = *ctx(t_dev < (int)g_devs.size() ? t_dev : 0);
+  std::lock_guard<std::mutex> lk(d.mu);
+  if (committee_keys) *committee_keys = d.cm_n;
+  if (auto_keys) *auto_keys = d.ak_n;
   return 0;
 }
 

@@ -18,6 +18,7 @@ extern "C" {
     pub fn nwc_verify_batch_many(digests: *const u8, offsets: *const u32, pks: *const u8, sigs: *const u8, m: usize,
                                  cert_ok_bitmap: *mut u8, bad_vote_bitmap: *mut u8) -> c_int;
     pub fn nwc_set_committee(pks: *const u8, n: usize) -> c_int;
+    pub fn nwc_cache_stats(committee_keys: *mut u32, auto_keys: *mut u32) -> c_int;
 
     pub fn nwc_set_committee_config(pks: *const u8, stakes: *const u64, n: usize, worker_offsets: *const u32,
                                     worker_ids: *const u32) -> c_int;
