@@ -961,10 +961,14 @@ struct TorsArgs {
   uint32_t* tflag;          // per slot: 1 = the key has torsion
   Committee committee;
   KeyMemo memo;
+  int pre;   // 1: mark/eval run before (or beside) the verification: every equation is a candidate,
+             //    k_tors_mark leaves the verdict words alone and k_tors_apply also applies the
+             //    committee flags
 };
-__device__ __forceinline__ bool tors_candidate(const TorsArgs& t, uint64_t idx, uint64_t& i, u32 aw[8], int& key) {
+__device__ __forceinline__ bool tors_candidate(const TorsArgs& t, uint64_t idx, uint64_t& i, u32 aw[8], int& key,
+                                               bool need_bit = true) {
   i = t.list ? (uint64_t)t.list[idx] : idx;
-  if (!((t.bits[i >> 6] >> (i & 63)) & 1)) return false;
+  if (need_bit && !((t.bits[i >> 6] >> (i & 63)) & 1)) return false;
   load_words8(t.pks + 32 * i, aw);
   key = committee_lookup(t.committee, aw);
   return true;
@@ -982,10 +986,10 @@ __global__ __launch_bounds__(256) void k_tors_mark(TorsArgs t) {
     uint64_t i;
     u32 aw[8];
     int key;
-    if (!tors_candidate(t, idx, i, aw, key)) continue;
+    if (!tors_candidate(t, idx, i, aw, key, !t.pre)) continue;
     const int known = key >= 0 ? (int)((t.committee.flags[key] & KEY_TORSION) != 0) : memo_lookup(t.memo, aw);
     if (known >= 0) {
-      if (known) atomicAnd(reinterpret_cast<unsigned long long*>(t.bits) + (i >> 6), ~(1ull << (i & 63)));
+      if (known && !t.pre) atomicAnd(reinterpret_cast<unsigned long long*>(t.bits) + (i >> 6), ~(1ull << (i & 63)));
       continue;
     }
     u32 h = committee_hash(aw[0], aw[1]) & t.slot_mask;
@@ -1021,7 +1025,12 @@ __global__ __launch_bounds__(256) void k_tors_apply(TorsArgs t) {
     uint64_t i;
     u32 aw[8];
     int key;
-    if (!tors_candidate(t, idx, i, aw, key) || key >= 0) continue;
+    if (!tors_candidate(t, idx, i, aw, key)) continue;
+    if (key >= 0) {   // cached key: its flag (k_tors_mark applied it unless pre)
+      if (t.pre && (t.committee.flags[key] & KEY_TORSION))
+        atomicAnd(reinterpret_cast<unsigned long long*>(t.bits) + (i >> 6), ~(1ull << (i & 63)));
+      continue;
+    }
     // memoised keys (found by k_tors_mark, or memoised by k_tors_eval just now) carry their flag;
     // clearing a bit k_tors_mark already cleared is harmless
     const int known = memo_lookup(t.memo, aw);

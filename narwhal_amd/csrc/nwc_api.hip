@@ -101,6 +101,8 @@ struct DevCtx {
   int cus = 0;
   int verify_blocks_per_cu = 1;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;      // small batch-leaf calls: the keys' torsion test beside the verification
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   nwc::ge_niels* base_table = nullptr;
   nwc::ge_niels_pad* base24 = nullptr;   // radix-2^24 basepoint tables (2.1 GB)
   nwc::ge_p3* base24_points = nullptr;    // B and 2^141 B
@@ -225,6 +227,9 @@ int init_device(DevCtx& d) {
     return set_err(NWC_ERR_NO_DEVICE, "device %d is %s; libnwc is built for gfx950 only", d.hip_id, prop.gcnArchName);
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&d.scratch_free, hipEventDisableTiming));
+  HIP_TRY(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
   d.cus = prop.multiProcessorCount;
   int bpc = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify<true, false>), 256, 0));
@@ -421,23 +426,29 @@ int ensure_scratch(DevCtx& d, size_t bytes, uint64_t n) {
 // (dalek verify_batch's randomized domain, answered Err; kernels.hip k_tors_*).  list/count
 // (device) restrict the pass to the comb path's uncached equations; nullptr = all n.  The hash set
 // is sized for the number of candidate equations, which never exceeds n <= fb_cap.
+// phase 1 = mark + eval, 2 = apply, 3 = both.  pre: phase 1 runs before or beside the
+// verification (every equation a candidate; the verdict words untouched until apply).
 int launch_torsion(DevCtx& d, const uint8_t* pks, uint64_t* out_words, uint64_t n, const uint32_t* list,
-                   const uint32_t* count, const nwc::Committee& cm, hipStream_t s) {
+                   const uint32_t* count, const nwc::Committee& cm, hipStream_t s, int phase = 3, int pre = 0) {
   if (n == 0) return 0;
   if (2 * n > d.ts_slot_count) return set_err(NWC_ERR_ARG, "torsion set too small for %llu equations", (unsigned long long)n);
-  HIP_TRY(hipMemsetAsync(d.ts_slots, 0xFF, 4 * (size_t)d.ts_slot_count, s));
-  HIP_TRY(hipMemsetAsync(d.ts_nuniq, 0, sizeof(uint32_t), s));
   const nwc::KeyMemo memo{d.km_keys, d.km_flag, NWC_MEMO_SLOTS - 1};
   const nwc::TorsArgs t{pks, out_words, list, count, n, d.ts_slots, d.ts_slot_count - 1, d.ts_uniq, d.ts_nuniq, d.ts_flag, cm,
-                        memo};
+                        memo, pre};
   const uint64_t cap = (uint64_t)d.cus * 8;
   const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, cap);
-  hipLaunchKernelGGL(nwc::k_tors_mark, dim3(grid), dim3(256), 0, s, t);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(nwc::k_tors_eval, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)d.cus * 2)), dim3(256), 0, s, t);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(nwc::k_tors_apply, dim3(grid), dim3(256), 0, s, t);
-  HIP_TRY(hipGetLastError());
+  if (phase & 1) {
+    HIP_TRY(hipMemsetAsync(d.ts_slots, 0xFF, 4 * (size_t)d.ts_slot_count, s));
+    HIP_TRY(hipMemsetAsync(d.ts_nuniq, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(nwc::k_tors_mark, dim3(grid), dim3(256), 0, s, t);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(nwc::k_tors_eval, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)d.cus * 2)), dim3(256), 0, s, t);
+    HIP_TRY(hipGetLastError());
+  }
+  if (phase & 2) {
+    hipLaunchKernelGGL(nwc::k_tors_apply, dim3(grid), dim3(256), 0, s, t);
+    HIP_TRY(hipGetLastError());
+  }
   return 0;
 }
 
@@ -501,6 +512,15 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
                     d.fb_list, d.fb_count, force_every, cm};
   const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
   const bool half = path != VPath::Full;
+  // small batch-leaf launches outside the comb path: the keys' torsion test (one long serial
+  // lane per new key) runs on the side stream beside the verification instead of after it
+  const bool tors_beside = !strict && !comb && n <= NWC_WIDE_MAX;
+  if (tors_beside) {
+    HIP_TRY(hipEventRecord(d.ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(d.side, d.ev_fork, 0));
+    if (int rc = launch_torsion(d, pks, out_words, n, nullptr, nullptr, cm, d.side, 1, 1)) return rc;
+    HIP_TRY(hipEventRecord(d.ev_join, d.side));
+  }
   if (half) HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
   if (comb) {
     HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
@@ -533,9 +553,13 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   }
   // batch leaves: keys with torsion (cached keys were checked in the comb kernels; the comb
   // path's other equations are its uncached list)
-  if (!strict)
+  if (tors_beside) {
+    HIP_TRY(hipStreamWaitEvent(s, d.ev_join, 0));
+    if (int rc = launch_torsion(d, pks, out_words, n, nullptr, nullptr, cm, s, 2, 1)) return rc;
+  } else if (!strict) {
     if (int rc = launch_torsion(d, pks, out_words, n, comb ? d.uc_list : nullptr, comb ? d.uc_count : nullptr, cm, s))
       return rc;
+  }
   HIP_TRY(hipEventRecord(d.scratch_free, s));
   return 0;
 }
@@ -785,6 +809,10 @@ void nwc_shutdown(void) {
     if (d->base_table) (void)hipFree(d->base_table);
     if (d->base24) (void)hipFree(d->base24);
     if (d->base24_points) (void)hipFree(d->base24_points);
+    if (d->side) (void)hipStreamSynchronize(d->side);
+    if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
+    if (d->ev_join) (void)hipEventDestroy(d->ev_join);
+    if (d->side) (void)hipStreamDestroy(d->side);
     if (d->stream) (void)hipStreamDestroy(d->stream);
   }
   g_devs.clear();
