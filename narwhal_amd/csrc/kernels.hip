@@ -501,10 +501,12 @@ __device__ __forceinline__ int base_window_digits(int w) {
 // latency hides behind ~2.6k VALU instructions and no VGPR holds the entry meanwhile.
 typedef __attribute__((address_space(1))) void nwc_gvoid;
 typedef __attribute__((address_space(3))) void nwc_lvoid;
-// NWC_STAGE_ENTRIES = 1 halves the stage (8 KB per wave) for occupancies above 2 waves per SIMD:
-// the second entry of a window is then fetched after the first one has been read.
+// NWC_STAGE_ENTRIES = 1 (default): an 8 KB stage per wave; the second entry of a window is
+// fetched after the first one has been read (it lands during the first Niels add).  Measured
+// +1.5 % verifies/s over a 16 KB two-entry stage (5 interleaved A/B pairs on two boxes,
+// profiles/r02/experiments.md), at the same occupancy (VGPR-bound to 2 waves per SIMD).
 #ifndef NWC_STAGE_ENTRIES
-#define NWC_STAGE_ENTRIES 2
+#define NWC_STAGE_ENTRIES 1
 #endif
 constexpr int STAGE_U4_PER_WAVE = NWC_STAGE_ENTRIES * 8 * 64;
 __device__ __forceinline__ void stage_fetch(uint4* stage, int e, const ge_niels_pad* src) {
@@ -847,7 +849,7 @@ __device__ __forceinline__ void stage_base_tables(const ge_niels* src, ge_niels*
 #endif
 template <bool HALF, bool CACHE, bool LIST = false>
 __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(VerifyArgs a, CombArgs ca) {
-  // HALF: per-wave LDS-DMA staging of radix-2^16 basepoint entries (64 KB per block);
+  // HALF: per-wave LDS-DMA staging of radix-2^24 basepoint entries (8 KB per wave);
   // full-length ladder: the radix-256 basepoint table (15.5 KB).
   __shared__ uint4 lds[HALF ? 4 * STAGE_U4_PER_WAVE : 129 * 30 / 4];
   ge_niels* sB = reinterpret_cast<ge_niels*>(lds);
