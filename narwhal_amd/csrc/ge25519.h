@@ -106,20 +106,46 @@ FE_DEV ge_niels ge_niels_cneg(const ge_niels& q, bool neg) {
 // The two 252-squaring exponentiations are serial chains; running A's and R's side by side gives
 // the scheduler two independent chains per lane.  Also returns the canonical y words (for the
 // small-order test).
+// Before the exponentiation: y, u = y^2 - 1, v^3 and z = u v^7 (v = d y^2 + 1).
+FE_DEV void ge_decompress_prep(const u32* w, fe& y, fe& u, fe& v3, fe& z) {
+  const fe one = fe_one();
+  y = fe_from_words(w);
+  const fe yy = fe_sq(y);
+  u = fe_sub(yy, one);
+  const fe v = fe_add(fe_mul(yy, FE_D), one);
+  v3 = fe_mul(fe_sq(v), v);
+  const fe v7 = fe_mul(fe_sq(v3), v);
+  z = fe_mul(u, v7);
+}
+// After it (b = z^((p-5)/8)): r = u v^3 b, the sqrt_ratio_i checks, sign fix-ups, the point.
+FE_DEV void ge_decompress_finish(const u32* w, const fe& y, const fe& u, const fe& v3, const fe& b, ge_p3& out,
+                                 u32 ycanon[8], bool& ok) {
+  const fe one = fe_one();
+  // r = u v^3 (u v^7)^((p-5)/8); check = v r^2
+  fe r = fe_mul(fe_mul(u, v3), b);
+  const fe yy = fe_sq(y);
+  const fe vv = fe_add(fe_mul(yy, FE_D), one);
+  fe check = fe_mul(vv, fe_sq(r));
+  const bool correct = fe_equal(check, u);
+  const bool flipped = fe_is_zero(fe_add(check, u));
+  const bool flipped_i = fe_is_zero(fe_add(check, fe_mul(u, FE_SQRTM1)));
+  r = fe_select(r, fe_mul(r, FE_SQRTM1), flipped || flipped_i);
+  r = fe_select(r, fe_neg(r), fe_is_negative(r));
+  const bool sign = (w[7] >> 31) & 1;
+  const fe x = fe_select(r, fe_neg(r), sign);
+  const fe yt = fe_tighten(y);
+  out.X = x;
+  out.Y = yt;
+  out.Z = one;
+  out.T = fe_mul(x, yt);
+  fe_to_words(y, ycanon);
+  ok = correct || flipped;
+}
+
 template <int N>
 FE_DEV void ge_decompressN(ge_p3 out[N], const u32* const w[N], u32 ycanon[N][8], bool ok[N]) {
   fe y[N], u[N], v[N], z[N];
-  const fe one = fe_one();
-  _Pragma("unroll") for (int k = 0; k < N; ++k) {
-    y[k] = fe_from_words(w[k]);
-    fe yy = fe_sq(y[k]);
-    u[k] = fe_sub(yy, one);
-    v[k] = fe_add(fe_mul(yy, FE_D), one);
-    fe v3 = fe_mul(fe_sq(v[k]), v[k]);
-    fe v7 = fe_mul(fe_sq(v3), v[k]);
-    z[k] = fe_mul(u[k], v7);
-    v[k] = v3;   // keep v^3 for r = u v^3 (u v^7)^((p-5)/8); v itself is recomputed below
-  }
+  _Pragma("unroll") for (int k = 0; k < N; ++k) ge_decompress_prep(w[k], y[k], u[k], v[k], z[k]);
   // z^(2^252 - 3) for both, interleaved
   fe a[N], b[N], t[N];
 #define BOTH(stmt) _Pragma("unroll") for (int k = 0; k < N; ++k) { stmt; }
@@ -151,27 +177,7 @@ FE_DEV void ge_decompressN(ge_p3 out[N], const u32* const w[N], u32 ycanon[N][8]
   BOTH(b[k] = fe_mul(b[k], t50[k]));                         // 2^250 - 1
   BOTH(b[k] = fe_mul(fe_sq(fe_sq(b[k])), z[k]));             // 2^252 - 3
 #undef BOTH
-  _Pragma("unroll") for (int k = 0; k < N; ++k) {
-    // r = u v^3 (u v^7)^((p-5)/8); check = v r^2
-    fe r = fe_mul(fe_mul(u[k], v[k]), b[k]);
-    const fe yy = fe_sq(y[k]);
-    const fe vv = fe_add(fe_mul(yy, FE_D), one);
-    fe check = fe_mul(vv, fe_sq(r));
-    const bool correct = fe_equal(check, u[k]);
-    const bool flipped = fe_is_zero(fe_add(check, u[k]));
-    const bool flipped_i = fe_is_zero(fe_add(check, fe_mul(u[k], FE_SQRTM1)));
-    r = fe_select(r, fe_mul(r, FE_SQRTM1), flipped || flipped_i);
-    r = fe_select(r, fe_neg(r), fe_is_negative(r));
-    const bool sign = (w[k][7] >> 31) & 1;
-    const fe x = fe_select(r, fe_neg(r), sign);
-    const fe yt = fe_tighten(y[k]);
-    out[k].X = x;
-    out[k].Y = yt;
-    out[k].Z = one;
-    out[k].T = fe_mul(x, yt);
-    fe_to_words(y[k], ycanon[k]);
-    ok[k] = correct || flipped;
-  }
+  _Pragma("unroll") for (int k = 0; k < N; ++k) ge_decompress_finish(w[k], y[k], u[k], v[k], b[k], out[k], ycanon[k], ok[k]);
 }
 
 // A decompressed point is small-order iff its y is one of the five y-coordinates of E[8]
