@@ -93,6 +93,10 @@ FES_DEV fes fes_mul(fes f, fes g) {
   return {live ? out : 0};
 }
 FES_DEV fes fes_sq(fes f) { return fes_mul(f, f); }
+FES_DEV fes fes_add(fes a, fes b) { return {a.v + b.v}; }
+FES_DEV fes fes_sub(fes a, fes b) { return {a.v - b.v}; }
+FES_DEV fes fes_add_small(fes a, i32 c) { return {fes_lane() == 0 ? a.v + c : a.v}; }   // + c (|c| small)
+FES_DEV fes fes_neg(fes a) { return {-a.v}; }
 
 FES_DEV fes fes_sqn(fes f, int n) {
   _Pragma("unroll 1") for (int i = 0; i < n; ++i) f = fes_sq(f);

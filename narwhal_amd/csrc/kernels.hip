@@ -829,6 +829,8 @@ struct CombArgs {
   uint32_t* count;
   const ge_niels_pad* comb_base;   // radix-256 basepoint comb (COMB_PER_KEY entries; latency kernel)
   const ge_niels_pad* comb16;      // radix-2^16 basepoint comb (COMB16_TOTAL entries; k_verify_comb)
+  uint8_t* vbytes;                 // latency kernel, host-mapped: per equation bit0 = valid, bit1 = key
+                                   // missing (plain byte stores; nullptr = verdict words + count)
 };
 
 __device__ __forceinline__ void load_inputs(const VerifyArgs& a, uint64_t i, u32 mw[8], u32 aw[8], u32 sgw[16]) {
@@ -1221,6 +1223,33 @@ __device__ __forceinline__ ge_p3 shfl_xor_p3(const ge_p3& p, int mask) {
   return r;
 }
 
+// R of the latency kernel: dalek's decompression (ge_decompress_prep / _finish) with every field
+// operation on the dependent chain limb-sliced; returns the affine x, y (Z = 1) as one element per
+// lane, the decode flag and the canonical y.
+__device__ __forceinline__ void decompress_sliced(const u32 w[8], fe& X, fe& Y, u32 ycanon[8], bool& ok) {
+  const fe yl = fe_from_words(w);
+  const fes y = fes_from_fe(yl);
+  const fes yy = fes_sq(y);
+  const fes u = fes_add_small(yy, -1);
+  const fes v = fes_add_small(fes_mul(yy, fes_from_fe(FE_D)), 1);
+  const fes v3 = fes_mul(fes_sq(v), v);
+  const fes v7 = fes_mul(fes_sq(v3), v);
+  const fes b = fes_pow22523(fes_mul(u, v7));
+  fes r = fes_mul(fes_mul(u, v3), b);                 // u v^3 (u v^7)^((p-5)/8)
+  const fes check = fes_mul(v, fes_sq(r));            // v r^2
+  const bool correct = fe_is_zero(fe_from_fes(fes_sub(check, u)));
+  const bool flipped = fe_is_zero(fe_from_fes(fes_add(check, u)));
+  const bool flipped_i = fe_is_zero(fe_from_fes(fes_add(check, fes_mul(u, fes_from_fe(FE_SQRTM1)))));
+  const fes ri = fes_mul(r, fes_from_fe(FE_SQRTM1));   // no branch: DPP must see every lane of the row
+  r.v = (flipped || flipped_i) ? ri.v : r.v;
+  fe rl = fe_from_fes(r);
+  rl = fe_select(rl, fe_neg(rl), fe_is_negative(rl));
+  X = fe_select(rl, fe_neg(rl), (w[7] >> 31) & 1);
+  Y = fe_tighten(yl);
+  fe_to_words(yl, ycanon);
+  ok = correct || flipped;
+}
+
 __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs ca) {
   __shared__ fe sh_rx, sh_ry;
   __shared__ int sh_rok;
@@ -1236,19 +1265,16 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
   _Pragma("unroll") for (int q = 0; q < 8; ++q) { rw[q] = sgw[q]; sw[q] = sgw[8 + q]; }
   ge_p3 sum;
   if (threadIdx.x >= 64) {
-    // wave 1: R (dalek decompression), its small-order flag.  The exponentiation -- this kernel's
+    // wave 1: R (dalek decompression), its small-order flag.  The decompression -- this kernel's
     // critical path -- runs limb-sliced (fe_sliced.h: one element per 16-lane row, 1.8x shorter
     // dependent chain); every row computes the same element.
-    ge_p3 R;
+    fe X, Y;
     u32 yc[8];
     bool ok;
-    fe y, u, v3, z;
-    ge_decompress_prep(rw, y, u, v3, z);
-    const fe b = fe_from_fes(fes_pow22523(fes_from_fe(z)));
-    ge_decompress_finish(rw, y, u, v3, b, R, yc, ok);
+    decompress_sliced(rw, X, Y, yc, ok);
     if (lane == 0) {
-      sh_rx = R.X;
-      sh_ry = R.Y;
+      sh_rx = X;
+      sh_ry = Y;
       sh_rok = ok && !(a.strict && ycanon_is_small_order(yc));
     }
   } else {
@@ -1276,11 +1302,16 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
     const u32 fl = cm.flags[kk];
     const bool flags_ok = key >= 0 && sc_lt_l(sw) && key_flags_ok(fl, a.strict != 0) && sh_rok;
     const bool eq = fe_is_zero(fe_sub(sum.X, fe_mul(sh_rx, sum.Z))) && fe_is_zero(fe_sub(sum.Y, fe_mul(sh_ry, sum.Z)));
-    if (key < 0) {
-      if (ca.list) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;
-      else atomicOr(ca.count, 1u);   // latency launch: flag it, the host re-runs the general path
+    if (ca.vbytes) {
+      // zero-copy latency launch: one byte per equation straight into pinned host memory
+      ca.vbytes[i] = (uint8_t)((flags_ok && eq ? 1u : 0u) | (key < 0 ? 2u : 0u));
+    } else {
+      if (key < 0) {
+        if (ca.list) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;
+        else atomicOr(ca.count, 1u);   // latency launch: flag it, the host re-runs the general path
+      }
+      if (flags_ok && eq) atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));
     }
-    if (flags_ok && eq) atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));
   }
 }
 

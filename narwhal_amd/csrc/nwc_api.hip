@@ -144,7 +144,8 @@ struct DevCtx {
   uint32_t cc_n = 0;
   uint8_t* msg_arena = nullptr;   // nwc_sanitize_messages buffers
   size_t msg_arena_cap = 0;
-  uint8_t* pinned = nullptr;   // host staging for small calls: one H2D and one D2H per call
+  uint8_t* pinned = nullptr;   // host staging for small calls: one H2D and one D2H per call, or
+  uint8_t* pinned_dev = nullptr;   // read in place by the latency kernel through this device pointer
   size_t pinned_cap = 0;
   // auto key cache (NWC_AUTO_KEYS): keys of small host calls outside the committee cache, added
   // with their flags, 129-entry tables and combs the second time they are seen, so that repeated
@@ -163,6 +164,9 @@ struct DevCtx {
     if (bytes <= pinned_cap) return 0;
     if (pinned) { (void)hipHostFree(pinned); pinned = nullptr; pinned_cap = 0; }
     HIP_TRY(hipHostMalloc(&pinned, bytes, hipHostMallocDefault));
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, pinned, 0));
+    pinned_dev = static_cast<uint8_t*>(dp);
     pinned_cap = bytes;
     return 0;
   }
@@ -458,7 +462,7 @@ constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4;   // LV_AUTO: t
 
 int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
-                  hipStream_t s, int flags = 0) {
+                  hipStream_t s, int flags = 0, uint8_t* vbytes = nullptr) {
   if (n == 0) return 0;
   const VPath path = verify_path();
   if ((flags & LV_AUTO) && (flags & LV_ALL_CACHED) && path == VPath::Default && n <= NWC_WIDE_MAX && d.ak_n) {
@@ -466,8 +470,9 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     const nwc::Committee cm{d.ak_keys, d.ak_flags, d.ak_tables, d.ak_comb, d.ak_slots, d.ak_host.mask, d.ak_n};
     const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24,
                             d.scratch, d.fb_list, d.fb_count, 0u, cm};
-    const nwc::CombArgs ca{nullptr, reinterpret_cast<uint32_t*>(out_words + (n + 63) / 64), d.comb_base, d.comb16};
-    if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64 + 1), s));
+    const nwc::CombArgs ca{nullptr, reinterpret_cast<uint32_t*>(out_words + (n + 63) / 64), d.comb_base, d.comb16,
+                           vbytes};
+    if (!vbytes && !(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64 + 1), s));
     hipLaunchKernelGGL(nwc::k_verify_comb_wide, dim3((unsigned)n), dim3(128), 0, s, a, ca);
     HIP_TRY(hipGetLastError());
     return 0;
@@ -481,8 +486,9 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
     const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24,
                             d.scratch, d.fb_list, d.fb_count, 0u, cm};
-    const nwc::CombArgs ca{nullptr, reinterpret_cast<uint32_t*>(out_words + (n + 63) / 64), d.comb_base, d.comb16};
-    if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64 + 1), s));
+    const nwc::CombArgs ca{nullptr, reinterpret_cast<uint32_t*>(out_words + (n + 63) / 64), d.comb_base, d.comb16,
+                           vbytes};
+    if (!vbytes && !(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64 + 1), s));
     hipLaunchKernelGGL(nwc::k_verify_comb_wide, dim3((unsigned)n), dim3(128), 0, s, a, ca);
     HIP_TRY(hipGetLastError());
     return 0;
@@ -676,11 +682,36 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     std::memcpy(h + (dp - d.arena), pks + 32 * lo, 32 * n);
     std::memcpy(h + (ds - d.arena), sigs + 64 * lo, 64 * n);
     std::memset(h + ((uint8_t*)dout - d.arena), 0, 8 * (words + 1));
-    HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena) + 8 * (words + 1), hipMemcpyHostToDevice,
-                           d.stream));
     int fl = LV_OUT_ZEROED;
     if (d.cm_n && g_hcm.all_cached(pks + 32 * lo, n)) fl |= LV_ALL_CACHED;
     else if (d.ak_n && n <= NWC_WIDE_MAX && d.ak_host.all_found(pks + 32 * lo, n)) fl |= LV_ALL_CACHED | LV_AUTO;
+    const size_t vb_off = align256(need);   // byte verdicts of a zero-copy launch, after the staged inputs
+    if ((fl & LV_ALL_CACHED) && n <= NWC_WIDE_MAX && vb_off + n <= NWC_PINNED_STAGE_MAX &&
+        verify_path() == VPath::Default && (fl & LV_AUTO ? d.ak_comb != nullptr : d.cm_comb != nullptr)) {
+      // every key cached: the latency kernel reads the staged inputs in place from pinned host
+      // memory and stores one verdict byte per equation there -- no DMA copy either way
+      uint8_t* hb = h + vb_off;
+      std::memset(hb, 0, n);
+      auto dev = [&](const void* p) { return p ? d.pinned_dev + ((const uint8_t*)p - d.arena) : nullptr; };
+      if (int rc = launch_verify(d, dev(dm), reinterpret_cast<const uint32_t*>(dev(dmi)), msg_stride ? 1 : 0, dev(dp),
+                                 dev(ds), n, strict, dout, d.stream, fl, d.pinned_dev + (hb - h)))
+        return rc;
+      HIP_TRY(hipStreamSynchronize(d.stream));
+      bool missing = false;
+      for (uint64_t i = 0; i < n; ++i) {
+        if (hb[i] & 1) out_words[i >> 6] |= 1ull << (i & 63);
+        missing = missing || (hb[i] & 2);
+      }
+      if (!missing) return 0;
+      // a key was missing on the device after all: stage the inputs and run the general path
+      std::fill(out_words.begin(), out_words.end(), 0);
+      fl &= ~(LV_ALL_CACHED | LV_AUTO);
+      HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena) + 8 * (words + 1), hipMemcpyHostToDevice,
+                             d.stream));
+    } else {
+      HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena) + 8 * (words + 1), hipMemcpyHostToDevice,
+                             d.stream));
+    }
     if (int rc = launch_verify(d, dm, dmi, msg_stride ? 1 : 0, dp, ds, n, strict, dout, d.stream, fl)) return rc;
     HIP_TRY(hipMemcpyAsync(h, dout, 8 * (words + 1), hipMemcpyDeviceToHost, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
