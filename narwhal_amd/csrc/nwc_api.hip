@@ -686,7 +686,11 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     if (d.cm_n && g_hcm.all_cached(pks + 32 * lo, n)) fl |= LV_ALL_CACHED;
     else if (d.ak_n && n <= NWC_WIDE_MAX && d.ak_host.all_found(pks + 32 * lo, n)) fl |= LV_ALL_CACHED | LV_AUTO;
     const size_t vb_off = align256(need);   // byte verdicts of a zero-copy launch, after the staged inputs
-    if ((fl & LV_ALL_CACHED) && n <= NWC_WIDE_MAX && vb_off + n <= NWC_PINNED_STAGE_MAX &&
+    static const bool zero_copy = [] {
+      const char* e = std::getenv("NWC_ZERO_COPY");
+      return !(e && std::strcmp(e, "0") == 0);
+    }();
+    if (zero_copy && (fl & LV_ALL_CACHED) && n <= NWC_WIDE_MAX && vb_off + n <= NWC_PINNED_STAGE_MAX &&
         verify_path() == VPath::Default && (fl & LV_AUTO ? d.ak_comb != nullptr : d.cm_comb != nullptr)) {
       // every key cached: the latency kernel reads the staged inputs in place from pinned host
       // memory and stores one verdict byte per equation there -- no DMA copy either way
