@@ -209,3 +209,30 @@ def test_comb_small_host_calls(lib, golden_verify, oracle):
             assert (rc == 0) == cases[i]["strict"]
     finally:
         _set_committee(lib, None)
+
+
+def test_latency_kernel_mutated_votes_vs_oracle(lib, oracle):
+    """The latency kernel (limb-sliced decompression of R, zero-copy call) on single votes through
+    the host ABI: random signature bit flips, wrong messages, s + l, small-order and non-canonical
+    R, flipped R sign bits and random R bytes (mostly non-decoding), against the oracle."""
+    from narwhal_amd import _lib
+    rng = np.random.default_rng(78)
+    N = 16
+    seeds = rng.integers(0, 256, (N, 32), dtype=np.uint8)
+    committee, _ = oracle.keygen_sign_many(seeds, np.zeros((N, 32), np.uint8))
+    m, p, s, _ = _mutated_committee_votes(oracle, rng, 1500, committee, seeds)
+    rnd = rng.random(len(s)) < 0.1
+    s[rnd, :32] = rng.integers(0, 256, (int(rnd.sum()), 32), dtype=np.uint8)   # arbitrary R bytes
+    exp_st = oracle.strict_many(m, p, s)
+    exp_lf = oracle.leaf_many(m, p, s)
+    try:
+        _set_committee(lib, committee)
+        for i in range(len(s)):
+            rc = _lib.check(lib.nwc_verify_strict(_lib.buf(m[i]), _lib.buf(p[i]), _lib.buf(s[i])))
+            assert (rc == 0) == exp_st[i], i
+            bad = ctypes.create_string_buffer(1)
+            rc = _lib.check(lib.nwc_verify_batch(_lib.buf(m[i]), _lib.buf(p[i]), _lib.buf(s[i]), 1, bad))
+            assert (rc == 0) == exp_lf[i], i
+        assert exp_st.sum() > 100 and (~exp_st).sum() > 100
+    finally:
+        _set_committee(lib, None)
