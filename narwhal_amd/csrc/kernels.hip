@@ -1259,11 +1259,10 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
   u32 mw[8], aw[8], sgw[16];
   load_inputs(a, i, mw, aw, sgw);
   const int lane = threadIdx.x & 63;
-  const int key = committee_lookup(cm, aw);
-  const int kk = key < 0 ? 0 : key;
   u32 rw[8], sw[8];
   _Pragma("unroll") for (int q = 0; q < 8; ++q) { rw[q] = sgw[q]; sw[q] = sgw[8 + q]; }
   ge_p3 sum;
+  int key = -1, kk = 0;   // wave 0 only: wave 1 (the critical path) starts on R at once
   if (threadIdx.x >= 64) {
     // wave 1: R (dalek decompression), its small-order flag.  The decompression -- this kernel's
     // critical path -- runs limb-sliced (fe_sliced.h: one element per 16-lane row, 1.8x shorter
@@ -1280,6 +1279,8 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
   } else {
     // lanes 0..31: basepoint comb (radix 2^8) windows; lanes 32..53: key comb (radix 2^12)
     // windows; lanes 54..63 hold the identity
+    key = committee_lookup(cm, aw);
+    kk = key < 0 ? 0 : key;
     u32 kw[8], sd[8], kd[9];
     challenge(rw, aw, mw, kw);
     sc_recode_radix256(sw, sd);

@@ -29,7 +29,7 @@ for i in range(n_calls + 100):
     t0 = time.perf_counter()
     rc = lib.nwc_verify_batch(_lib.buf(d), _lib.buf(p), _lib.buf(s), 3, None)
     dt = time.perf_counter() - t0
-    assert rc == 0
+    assert rc == 0 or os.environ.get("NWC_LAT_ANY"), rc
     if i >= 100:
         lat[i - 100] = dt * 1e6
 q = np.percentile(lat, [50, 90, 99, 99.9])
