@@ -18,6 +18,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "nwc.h"
@@ -157,7 +158,7 @@ struct DevCtx {
   int32_t* ak_slots = nullptr;
   uint32_t ak_n = 0, ak_cap = 0, ak_slot_cap = 0;
   KeyIndex ak_host;                       // host copy of the auto cache's lookup table
-  std::vector<nwc::u32> ak_seen;          // keys seen once (8 words each), bounded
+  std::unordered_set<std::string> ak_seen;   // keys seen once (32-byte strings), bounded
   std::mutex mu;
 
   int ensure_pinned(size_t bytes) {
@@ -298,19 +299,19 @@ int auto_insert(DevCtx& d, const uint8_t* pks, uint64_t n) {
   const uint32_t cap = auto_keys_cap();
   if (cap == 0 || d.ak_n >= cap) return 0;
   std::vector<nwc::u32> add;
+  std::unordered_set<std::string> added;
   for (uint64_t i = 0; i < n && d.ak_n + add.size() / 8 < cap; ++i) {
     const uint8_t* k = pks + 32 * i;
     if (d.ak_host.find(k)) continue;
-    bool dup = false;
-    for (size_t j = 0; j < add.size() && !dup; j += 8) dup = std::memcmp(&add[j], k, 32) == 0;
-    if (dup) continue;
-    bool seen = false;
-    for (size_t j = 0; j < d.ak_seen.size() && !seen; j += 8) seen = std::memcmp(&d.ak_seen[j], k, 32) == 0;
-    if (!seen) {
-      if (d.ak_seen.size() >= 8 * AUTO_SEEN_MAX) d.ak_seen.clear();
-      d.ak_seen.insert(d.ak_seen.end(), reinterpret_cast<const nwc::u32*>(k), reinterpret_cast<const nwc::u32*>(k) + 8);
+    std::string ks(reinterpret_cast<const char*>(k), 32);
+    if (added.count(ks)) continue;
+    if (!d.ak_seen.count(ks)) {
+      if (d.ak_seen.size() >= AUTO_SEEN_MAX) d.ak_seen.clear();
+      d.ak_seen.insert(std::move(ks));
       continue;
     }
+    d.ak_seen.erase(ks);
+    added.insert(ks);
     add.insert(add.end(), reinterpret_cast<const nwc::u32*>(k), reinterpret_cast<const nwc::u32*>(k) + 8);
   }
   const uint32_t m = (uint32_t)(add.size() / 8);
