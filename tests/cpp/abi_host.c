@@ -6,13 +6,50 @@
  *   S <msg32> <pk32> <sig64>            -> "S <rc>"                 (nwc_verify_strict)
  *   B <msg32> <n> <pk32 sig64> x n      -> "B <rc> <bad bitmap>"    (nwc_verify_batch)
  *   D <data>                            -> "D <digest32>"           (nwc_sha512_trunc32_many)
- * Built by __graft_entry__.build() into tests/cpp/build/abi_host; run by tests/test_gpu_abi_host.py.
+ *   V <n>, then n lines <msg32 pk32 sig64>  -> "V <rc> <bitmap>"     (nwc_verify_strict_many)
+ *   C <m> <offsets m+1>, then offsets[m] vote lines <digest-index pk32 sig64> and m digest lines
+ *                                       -> "C <rc> <cert bitmap> <bad bitmap>" (nwc_verify_batch_many)
+ *   X <threads> <rounds>                -> "X <mismatches>": every B request so far re-run from
+ *                                          that many concurrent host threads, results compared
+ *   Z                                   -> a heap read one byte out of bounds (sanitizer self-check)
+ * Built by __graft_entry__.build() into tests/cpp/build/abi_host (and, host code under
+ * AddressSanitizer + UBSan against a sanitized libnwc, abi_host_asan); run by
+ * tests/test_gpu_abi_host.py.
  */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "nwc.h"
+
+/* B requests kept for the X (concurrency) command */
+typedef struct {
+  unsigned char m[32];
+  unsigned char* pks;
+  unsigned char* sigs;
+  size_t n;
+  int rc;
+  unsigned char* bad;
+} breq;
+static breq g_b[4096];
+static size_t g_nb;
+static int g_rounds;
+
+static void* worker(void* arg) {
+  long bad_count = 0;
+  (void)arg;
+  for (int r = 0; r < g_rounds; ++r) {
+    for (size_t i = 0; i < g_nb; ++i) {
+      const breq* q = &g_b[i];
+      unsigned char* bad = calloc(q->n / 8 + 1, 1);
+      const int rc = nwc_verify_batch(q->m, q->pks, q->sigs, q->n, bad);
+      if (rc != q->rc || memcmp(bad, q->bad, (q->n + 7) / 8) != 0) ++bad_count;
+      free(bad);
+    }
+  }
+  return (void*)bad_count;
+}
 
 static int unhex(const char* s, unsigned char* out, size_t n) {
   if (strlen(s) != 2 * n) return -1;
@@ -63,9 +100,102 @@ int main(void) {
       printf("B %d ", rc);
       puthex(bad, (n + 7) / 8);
       printf("\n");
+      if (g_nb < sizeof g_b / sizeof g_b[0]) {
+        breq* q = &g_b[g_nb++];
+        memcpy(q->m, m, 32);
+        q->pks = pks;
+        q->sigs = sigs;
+        q->n = n;
+        q->rc = rc;
+        q->bad = bad;
+      } else {
+        free(pks);
+        free(sigs);
+        free(bad);
+      }
+    } else if (tok[0] == 'V') {
+      const char* cnt = strtok(NULL, " \n");
+      if (!cnt) return 3;
+      const size_t n = (size_t)strtoul(cnt, NULL, 10);
+      unsigned char* ms = malloc(32 * n + 1);
+      unsigned char* pks = malloc(32 * n + 1);
+      unsigned char* sigs = malloc(64 * n + 1);
+      unsigned char* bits = calloc(n / 8 + 1, 1);
+      for (size_t i = 0; i < n; ++i) {
+        if (!fgets(line, sizeof line, stdin)) return 3;
+        const char* a = strtok(line, " \n");
+        const char* b = strtok(NULL, " \n");
+        const char* c = strtok(NULL, " \n");
+        if (!a || !b || !c || unhex(a, ms + 32 * i, 32) || unhex(b, pks + 32 * i, 32) || unhex(c, sigs + 64 * i, 64))
+          return 3;
+      }
+      rc = nwc_verify_strict_many(ms, pks, sigs, n, bits);
+      printf("V %d ", rc);
+      puthex(bits, (n + 7) / 8);
+      printf("\n");
+      free(ms);
       free(pks);
       free(sigs);
-      free(bad);
+      free(bits);
+    } else if (tok[0] == 'C') {
+      const char* cnt = strtok(NULL, " \n");
+      if (!cnt) return 3;
+      const size_t mc = (size_t)strtoul(cnt, NULL, 10);
+      uint32_t* offs = malloc(4 * (mc + 1));
+      for (size_t c = 0; c <= mc; ++c) {
+        const char* o = strtok(NULL, " \n");
+        if (!o) return 3;
+        offs[c] = (uint32_t)strtoul(o, NULL, 10);
+      }
+      const size_t nv = offs[mc];
+      unsigned char* pks = malloc(32 * nv + 1);
+      unsigned char* sigs = malloc(64 * nv + 1);
+      unsigned char* dig = malloc(32 * mc + 1);
+      for (size_t i = 0; i < nv; ++i) {
+        if (!fgets(line, sizeof line, stdin)) return 3;
+        const char* b = strtok(line, " \n");
+        const char* c = strtok(NULL, " \n");
+        if (!b || !c || unhex(b, pks + 32 * i, 32) || unhex(c, sigs + 64 * i, 64)) return 3;
+      }
+      for (size_t c = 0; c < mc; ++c) {
+        if (!fgets(line, sizeof line, stdin)) return 3;
+        const char* a = strtok(line, " \n");
+        if (!a || unhex(a, dig + 32 * c, 32)) return 3;
+      }
+      unsigned char* cert = calloc(mc / 8 + 1, 1);
+      unsigned char* badv = calloc(nv / 8 + 1, 1);
+      rc = nwc_verify_batch_many(dig, offs, pks, sigs, mc, cert, badv);
+      printf("C %d ", rc);
+      puthex(cert, (mc + 7) / 8);
+      printf(" ");
+      puthex(badv, (nv + 7) / 8);
+      printf("\n");
+      free(offs);
+      free(pks);
+      free(sigs);
+      free(dig);
+      free(cert);
+      free(badv);
+    } else if (tok[0] == 'X') {
+      const char* t = strtok(NULL, " \n");
+      const char* r = strtok(NULL, " \n");
+      if (!t || !r) return 3;
+      const int threads = atoi(t);
+      g_rounds = atoi(r);
+      pthread_t th[64];
+      long mism = 0;
+      for (int k = 0; k < threads && k < 64; ++k) pthread_create(&th[k], NULL, worker, NULL);
+      for (int k = 0; k < threads && k < 64; ++k) {
+        void* v = NULL;
+        pthread_join(th[k], &v);
+        mism += (long)v;
+      }
+      printf("X %ld\n", mism);
+    } else if (tok[0] == 'Z') {
+      /* sanitizer self-check (tests only): one byte read past a heap block must be reported */
+      volatile unsigned char* z = malloc(16);
+      printf("Z %d\n", z[16]);
+      free((void*)z);
     } else if (tok[0] == 'D') {
       const char* a = strtok(NULL, " \n");
       const size_t len = a ? strlen(a) / 2 : 0;
@@ -84,6 +214,11 @@ int main(void) {
       free(data);
     }
     fflush(stdout);
+  }
+  for (size_t i = 0; i < g_nb; ++i) {
+    free(g_b[i].pks);
+    free(g_b[i].sigs);
+    free(g_b[i].bad);
   }
   nwc_shutdown();
   return 0;

@@ -12,14 +12,35 @@ from tests.conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 BIN = os.path.join(ROOT, "tests", "cpp", "build", "abi_host")
+ASAN_BIN = os.path.join(ROOT, "tests", "cpp", "build", "abi_host_asan")
+ASAN_LIB = os.path.join(ROOT, "tests", "cpp", "build", "libnwc_asan.so")
+
+
+def _stale(out, srcs):
+    return not os.path.exists(out) or any(os.path.getmtime(x) > os.path.getmtime(out) for x in srcs)
 
 
 def build_abi_host() -> str:
-    """gcc, linked against the in-tree libnwc.so (rpath relative to the binary)."""
+    """gcc, linked against the in-tree libnwc.so (rpath relative to the binary); and the sanitized
+    pair: libnwc's HOST code under AddressSanitizer + UBSan (`-Xarch_host -fsanitize=...`; the
+    gfx950 device code is built as usual) with the same C host built by ROCm's clang."""
     os.makedirs(os.path.dirname(BIN), exist_ok=True)
-    subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-I" + os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "cpp", "abi_host.c"), "-L" + os.path.join(ROOT, "narwhal_amd"),
-                    "-l:libnwc.so", "-Wl,-rpath,$ORIGIN/../../../narwhal_amd", "-o", BIN], check=True)
+    src = os.path.join(ROOT, "tests", "cpp", "abi_host.c")
+    inc = "-I" + os.path.join(ROOT, "include")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", inc, src, "-L" + os.path.join(ROOT, "narwhal_amd"),
+                    "-l:libnwc.so", "-lpthread", "-Wl,-rpath,$ORIGIN/../../../narwhal_amd", "-o", BIN], check=True)
+    from narwhal_amd import build as nb
+    if _stale(ASAN_LIB, nb.sources()):
+        subprocess.run([nb.HIPCC, "--offload-arch=gfx950", "-O2", "-g", "-std=c++20", "-fPIC", "-shared",
+                        "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+                        "-Xarch_host", "-fno-sanitize-recover=undefined", inc, "-I" + nb.CSRC,
+                        "-o", ASAN_LIB + ".tmp", os.path.join(nb.CSRC, "nwc_api.hip")], check=True)
+        os.replace(ASAN_LIB + ".tmp", ASAN_LIB)
+    if _stale(ASAN_BIN, [src, ASAN_LIB]):
+        subprocess.run(["/opt/rocm/llvm/bin/clang", "-O1", "-g", "-fsanitize=address,undefined",
+                        "-fno-sanitize-recover=undefined", inc, src, "-L" + os.path.dirname(ASAN_LIB),
+                        "-l:" + os.path.basename(ASAN_LIB), "-lpthread", "-Wl,-rpath,$ORIGIN", "-o", ASAN_BIN],
+                       check=True)
     return BIN
 
 
@@ -48,3 +69,62 @@ def test_c_host_golden(golden_verify, golden_batch, golden_sha):
     assert len(got) == len(want), (len(got), len(want))
     bad = [(i, g, w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
     assert not bad, bad[:5]
+
+
+def test_c_host_under_asan(oracle, golden_verify, golden_batch):
+    """libnwc's host code (small-call staging, zero-copy path, auto key cache, shard threads and
+    bitmap merges over NWC_VIRTUAL_DEVICES=3 contexts, certificate cuts, concurrent callers)
+    under AddressSanitizer + UBSan: no report, and every output equal to the oracle's."""
+    import numpy as np
+    if _stale(ASAN_BIN, [ASAN_LIB]):
+        build_abi_host()
+    rng = np.random.default_rng(41)
+    lines, want = [], []
+    for b in golden_batch:
+        n = len(b["votes"])
+        lines.append("B %s %d %s" % (b["msg"], n, " ".join("%s %s" % (p, s) for p, s in b["votes"])))
+        bits = bytearray((n + 7) // 8)
+        for i in b["bad"]:
+            bits[i >> 3] |= 1 << (i & 7)
+        want.append(("B %d %s" % (0 if b["verdict"] else 1, bits.hex())).rstrip())
+    # sharded strict verification: 9001 triples over three contexts, flips around the cuts
+    n = 9001
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pks, sigs = oracle.keygen_sign_many(seeds, msgs)
+    flip = rng.random(n) < 0.03
+    flip[[0, 63, 64, 3000, 3007, 3008, 6015, 6016, n - 1]] = True
+    sigs[flip, 40] ^= 2
+    lines.append("V %d" % n)
+    lines += ["%s %s %s" % (m.tobytes().hex(), p.tobytes().hex(), s.tobytes().hex()) for m, p, s in zip(msgs, pks, sigs)]
+    exp = oracle.strict_many(msgs, pks, sigs)
+    want.append("V 0 " + np.packbits(exp, bitorder="little").tobytes().hex())
+    # certificates: 0..40 votes each over one digest per certificate
+    sizes = [int(x) for x in rng.integers(0, 41, 200)]
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    nv = int(offs[-1])
+    dig = rng.integers(0, 256, (len(sizes), 32), dtype=np.uint8)
+    vm = np.repeat(dig, sizes, axis=0)
+    vp, vs = oracle.keygen_sign_many(seeds[:nv], vm)
+    bad = rng.random(nv) < 0.05
+    vs[bad, 50] ^= 8
+    lines.append("C %d %s" % (len(sizes), " ".join(str(int(o)) for o in offs)))
+    lines += ["%s %s" % (p.tobytes().hex(), s.tobytes().hex()) for p, s in zip(vp, vs)]
+    lines += [d.tobytes().hex() for d in dig]
+    ocert, obad = oracle.batch_many(dig, offs, vp, vs)
+    want.append("C 0 %s %s" % (np.packbits(ocert, bitorder="little").tobytes().hex(),
+                               np.packbits(obad, bitorder="little").tobytes().hex()))
+    lines.append("X 4 3")
+    want.append("X 0")
+    env = dict(os.environ, NWC_VIRTUAL_DEVICES="3", ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([ASAN_BIN], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.returncode, r.stdout[-500:], r.stderr[-3000:])
+    assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+    got = [l.rstrip() for l in r.stdout.splitlines()]
+    assert len(got) == len(want), (len(got), len(want), r.stderr[-1000:])
+    mism = [(i, g[:80], w[:80]) for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not mism, mism[:5]
+    # the sanitizer is live in this process layout: an out-of-bounds heap read is reported
+    r = subprocess.run([ASAN_BIN], input="Z\n", capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "heap-buffer-overflow" in r.stderr, (r.returncode, r.stderr[-500:])
