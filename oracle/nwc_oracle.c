@@ -356,7 +356,7 @@ static void slide(signed char naf[257], const u8 k[32], int w) {
   int pos = 0;
   const int W = 1 << w, H = 1 << (w - 1);
   while (pos < 257) {
-    int nz = x[0] | x[1] | x[2] | x[3] | x[4];
+    const u64 nz = x[0] | x[1] | x[2] | x[3] | x[4];   /* u64: an int truncation ended the NAF early */
     if (!nz) break;
     if (x[0] & 1) {
       int d = (int)(x[0] & (u64)(W - 1));

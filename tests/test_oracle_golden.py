@@ -177,3 +177,22 @@ def test_straus_port_over_golden_cases(oracle, golden_verify, golden_batch):
             assert acc == 0, (name, acc)
         else:
             assert 0 < acc <= D // 2 + 30, (name, acc)
+
+
+def test_c_oracle_naf_regression():
+    """A valid signature (OpenSSL and the Python restatement accept it) whose s has a run of 32
+    one-bits: the C oracle's w-NAF used to test `x != 0` through an int truncation of the 64-bit
+    words, stopped early and rejected it (found by tools/soak.py, 8M triples against the GPU)."""
+    from tests.oracle_lib import load_oracle
+    import ed25519_ref as ref
+    m = bytes.fromhex("adbf69bd12f7b78ae103e1e15e21cfa0e862d2e492dc98155ccec3ad8e16f625")
+    p = bytes.fromhex("45e29965903c8cd825088deda51115e3ae0ee8db818b5f231422385ab925d06d")
+    s = bytes.fromhex("835f54b9c9c8428222c49fa397001beb077b13522f721df5466496e5ea7974fe"
+                      "17ac23fc48581fce3c62560bd50ff419c4b17653a715f34ef3ffffff8fed7a03")
+    assert ref.verify_strict(m, p, s)
+    o = load_oracle()
+    assert o.verify_strict(m, p, s) and o.leaf(m, p, s)
+    # and a batch (the Straus port shares the NAF)
+    import numpy as np
+    assert o.batch_straus_many(np.frombuffer(m, np.uint8).reshape(1, 32), np.array([0, 1], np.uint32),
+                               np.frombuffer(p, np.uint8).reshape(1, 32), np.frombuffer(s, np.uint8).reshape(1, 64)).all()

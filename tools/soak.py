@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""Differential soak: N synthetic (msg, pk, sig) triples, mutated into every input class the path
+has (bit flips in R / s / A / msg, s + l, small-order and non-canonical R and A encodings, random R
+and A bytes, the golden edge cases tiled in), verified on the GPU in strict and batch-leaf mode
+and compared verdict by verdict with the CPU restatement (oracle/, multithreaded).
+
+    python tools/soak.py [--n 8388608] [--chunk 1048576] [--out gpurun_out/soak.json]
+
+Prints one JSON object: per class counts, valid counts and mismatches (must be 0)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+from narwhal_amd import _lib, device  # noqa: E402
+from tests.oracle_lib import load_oracle  # noqa: E402
+
+P = (1 << 255) - 19
+L = (1 << 252) + 27742317777372353535851937790883648493
+Y8 = 0x05fc536d880238b13933c6d305acdfd5f098eff289f4c345b027b2c28f95e826   # y of the order-8 points
+
+
+def enc(y: int, sign: int) -> bytes:
+    return (y | (sign << 255)).to_bytes(32, "little")
+
+
+SMALL = [enc(y, s) for y in (0, 1, P - 1, Y8, P - Y8) for s in (0, 1)] + \
+        [enc(y + P, s) for y in (0, 1) for s in (0, 1)]   # non-canonical aliases y + p < 2^255
+CLASSES = ["valid", "flip_R", "flip_s", "flip_A", "flip_msg", "s_plus_l", "small_R", "small_A",
+           "random_R", "random_A", "noncanon_R", "golden"]
+
+
+def mutate(rng, m, p, s, golden):
+    n = len(p)
+    kind = rng.choice(len(CLASSES), n, p=[0.30, 0.07, 0.07, 0.07, 0.07, 0.06, 0.06, 0.06, 0.06, 0.06, 0.06, 0.06])
+    idx = lambda k: np.nonzero(kind == k)[0]  # noqa: E731
+    i = idx(1); s[i, rng.integers(0, 32, len(i))] ^= (1 << rng.integers(0, 8, len(i))).astype(np.uint8)
+    i = idx(2); s[i, 32 + rng.integers(0, 32, len(i))] ^= (1 << rng.integers(0, 8, len(i))).astype(np.uint8)
+    i = idx(3); p[i, rng.integers(0, 32, len(i))] ^= (1 << rng.integers(0, 8, len(i))).astype(np.uint8)
+    i = idx(4); m[i, rng.integers(0, 32, len(i))] ^= (1 << rng.integers(0, 8, len(i))).astype(np.uint8)
+    for j in idx(5):
+        sv = int.from_bytes(s[j, 32:].tobytes(), "little") + L
+        if sv < (1 << 256):
+            s[j, 32:] = np.frombuffer(sv.to_bytes(32, "little"), np.uint8)
+    small = np.frombuffer(b"".join(SMALL), np.uint8).reshape(-1, 32)
+    i = idx(6); s[i, :32] = small[rng.integers(0, len(small), len(i))]
+    i = idx(7); p[i] = small[rng.integers(0, len(small), len(i))]
+    i = idx(8); s[i, :32] = rng.integers(0, 256, (len(i), 32), dtype=np.uint8)
+    i = idx(9); p[i] = rng.integers(0, 256, (len(i), 32), dtype=np.uint8)
+    for j in idx(10):   # same R point, non-canonical encoding when y + p fits (rare for random y)
+        y = int.from_bytes(s[j, :32].tobytes(), "little")
+        yy, sign = y & ((1 << 255) - 1), y >> 255
+        if yy + P < (1 << 255):
+            s[j, :32] = np.frombuffer(enc(yy + P, sign), np.uint8)
+        else:
+            s[j, 31] ^= 0x80   # else flip the sign bit
+    gm, gp, gs = golden
+    i = idx(11); g = rng.integers(0, len(gm), len(i)); m[i], p[i], s[i] = gm[g], gp[g], gs[g]
+    return kind
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8 << 20)
+    ap.add_argument("--chunk", type=int, default=1 << 20)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "soak.json"))
+    args = ap.parse_args()
+    lib = _lib.load()
+    orc = load_oracle()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "ed25519_verify.json")))
+    cases = [c for c in gold["cases"] if len(c["msg"]) == 64]
+    golden = tuple(np.stack([np.frombuffer(bytes.fromhex(c[k]), np.uint8) for c in cases]) for k in ("msg", "pk", "sig"))
+    rng = np.random.default_rng(20261016)
+    stats = {c: {"n": 0, "strict_valid": 0, "leaf_valid": 0, "strict_mismatch": 0, "leaf_mismatch": 0} for c in CLASSES}
+    t0 = time.time()
+    done = 0
+    mism = []
+    while done < args.n:
+        n = min(args.chunk, args.n - done)
+        seeds = device.derive32(b"soak-seed", done, n)
+        msgs = device.derive32(b"soak-msg", done, n)
+        pks, sigs = device.keygen_sign(seeds, msgs)
+        torch.cuda.synchronize()
+        m, p, s = (t.cpu().numpy().copy() for t in (msgs, pks, sigs))
+        kind = mutate(rng, m, p, s, golden)
+        tm, tp, ts = (torch.from_numpy(x).cuda() for x in (m, p, s))
+        gs = device.unpack_bits(device.verify(tm, tp, ts, strict=True), n)
+        gl = device.unpack_bits(device.verify(tm, tp, ts, strict=False), n)
+        os_ = orc.strict_many(m, p, s, threads=threads)
+        ol = orc.leaf_many(m, p, s, threads=threads)
+        for j in np.nonzero((gs != os_) | (gl != ol))[0][:20]:
+            mism.append({"class": CLASSES[kind[j]], "index": int(done + j), "msg": m[j].tobytes().hex(),
+                         "pk": p[j].tobytes().hex(), "sig": s[j].tobytes().hex(), "gpu_strict": bool(gs[j]),
+                         "oracle_strict": bool(os_[j]), "gpu_leaf": bool(gl[j]), "oracle_leaf": bool(ol[j])})
+        for k, name in enumerate(CLASSES):
+            sel = kind == k
+            st = stats[name]
+            st["n"] += int(sel.sum())
+            st["strict_valid"] += int(os_[sel].sum())
+            st["leaf_valid"] += int(ol[sel].sum())
+            st["strict_mismatch"] += int((gs[sel] != os_[sel]).sum())
+            st["leaf_mismatch"] += int((gl[sel] != ol[sel]).sum())
+        done += n
+        print("soak %d / %d  %.0f s" % (done, args.n, time.time() - t0), file=sys.stderr, flush=True)
+    total = {k: sum(v[k] for v in stats.values()) for k in ("n", "strict_mismatch", "leaf_mismatch")}
+    out = {"triples": args.n, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
+           "mismatches": mism}
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    json.dump(out, open(args.out, "w"), indent=1)
+    print(json.dumps(total))
+    return 0 if total["strict_mismatch"] == 0 and total["leaf_mismatch"] == 0 else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
