@@ -70,8 +70,17 @@ def main():
     ap.add_argument("--n", type=int, default=8 << 20)
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "soak.json"))
+    ap.add_argument("--committee", type=int, default=0,
+                    help="K > 0: signers drawn from K keys registered with nwc_set_committee (comb path, "
+                         "cached ladder and the uncached list for mutated keys)")
     args = ap.parse_args()
     lib = _lib.load()
+    if args.committee:
+        cseeds = device.derive32(b"soak-seed", 0, args.committee)
+        cpks, _ = device.keygen_sign(cseeds, cseeds)
+        torch.cuda.synchronize()
+        ck = cpks.cpu().numpy().copy()
+        _lib.check(lib.nwc_set_committee(_lib.buf(ck), args.committee))
     orc = load_oracle()
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "ed25519_verify.json")))
@@ -84,7 +93,11 @@ def main():
     mism = []
     while done < args.n:
         n = min(args.chunk, args.n - done)
-        seeds = device.derive32(b"soak-seed", done, n)
+        if args.committee:
+            who = torch.from_numpy(rng.integers(0, args.committee, n)).cuda()
+            seeds = cseeds[who]
+        else:
+            seeds = device.derive32(b"soak-seed", done, n)
         msgs = device.derive32(b"soak-msg", done, n)
         pks, sigs = device.keygen_sign(seeds, msgs)
         torch.cuda.synchronize()
@@ -110,7 +123,7 @@ def main():
         done += n
         print("soak %d / %d  %.0f s" % (done, args.n, time.time() - t0), file=sys.stderr, flush=True)
     total = {k: sum(v[k] for v in stats.values()) for k in ("n", "strict_mismatch", "leaf_mismatch")}
-    out = {"triples": args.n, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
+    out = {"triples": args.n, "committee": args.committee, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
            "mismatches": mism}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(out, open(args.out, "w"), indent=1)
