@@ -4,7 +4,10 @@ has (bit flips in R / s / A / msg, s + l, small-order and non-canonical R and A 
 and A bytes, the golden edge cases tiled in), verified on the GPU in strict and batch-leaf mode
 and compared verdict by verdict with the CPU restatement (oracle/, multithreaded).
 
-    python tools/soak.py [--n 8388608] [--chunk 1048576] [--out gpurun_out/soak.json]
+    python tests/soak.py [--n 8388608] [--chunk 1048576] [--committee K] [--out gpurun_out/soak.json]
+
+Test infrastructure (it runs the oracle), kept under tests/ like the oracle helpers; not part of
+the default pytest run (minutes of CPU oracle time).
 
 Prints one JSON object: per class counts, valid counts and mismatches (must be 0)."""
 import argparse

@@ -182,7 +182,7 @@ def test_straus_port_over_golden_cases(oracle, golden_verify, golden_batch):
 def test_c_oracle_naf_regression():
     """A valid signature (OpenSSL and the Python restatement accept it) whose s has a run of 32
     one-bits: the C oracle's w-NAF used to test `x != 0` through an int truncation of the 64-bit
-    words, stopped early and rejected it (found by tools/soak.py, 8M triples against the GPU)."""
+    words, stopped early and rejected it (found by tests/soak.py, 8M triples against the GPU)."""
     from tests.oracle_lib import load_oracle
     import ed25519_ref as ref
     m = bytes.fromhex("adbf69bd12f7b78ae103e1e15e21cfa0e862d2e492dc98155ccec3ad8e16f625")
