@@ -325,6 +325,44 @@ struct LaneTable {
 };
 static_assert(sizeof(ge_cached) == TAB_U4_PER_ENTRY * 16, "cached point layout");
 
+// Coordinate k (0 YpX, 1 YmX, 2 Z, 3 T2d) of entry e: 40 bytes at an 8-byte-aligned offset.
+__device__ __forceinline__ fe lt_load_fe(const LaneTable& tab, int e, int k) {
+  const uint2* q = reinterpret_cast<const uint2*>(tab.p) + e * 20 + k * 5;
+  fe r;
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) {
+    const uint2 v = q[i];
+    r.v[2 * i] = (i32)v.x;
+    r.v[2 * i + 1] = (i32)v.y;
+  }
+  return r;
+}
+
+// t + (neg ? -q : q) for q = tab[e], t completed (p1p1), result completed: 8M, with the entry
+// read coordinate by coordinate and the extended form built pairwise, so at most ~2 points'
+// worth of field elements are live (the 3-waves-per-SIMD register budget).  -q swaps Y+X / Y-X
+// (a per-lane address choice) and negates 2dT (the sign flips on the sum/difference of zz2, tt).
+__device__ __forceinline__ ge_p1p1 add_lt(const ge_p1p1& t, const LaneTable& tab, int e, bool neg) {
+  const fe qa = lt_load_fe(tab, e, neg ? 1 : 0);
+  const fe qb = lt_load_fe(tab, e, neg ? 0 : 1);
+  const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Y, t.Z);
+  const fe a = fe_add(Y3, X3), b = fe_sub(Y3, X3);
+  const fe Z3 = fe_mul(t.Z, t.T), T3 = fe_mul(t.X, t.Y);
+  __builtin_amdgcn_sched_barrier(0);
+  const fe qz = lt_load_fe(tab, e, 2);
+  const fe qt = lt_load_fe(tab, e, 3);
+  const fe pp = fe_mul(a, qa), mm = fe_mul(b, qb);
+  ge_p1p1 r;
+  r.X = fe_sub(pp, mm);
+  r.Y = fe_add(pp, mm);
+  const fe zz = fe_mul(Z3, qz);
+  const fe zz2 = fe_add(zz, zz);
+  fe tt = fe_mul(T3, qt);
+  tt = fe_select(tt, fe_neg(tt), neg);
+  r.Z = fe_add(zz2, tt);
+  r.T = fe_sub(zz2, tt);
+  return r;
+}
+
 // tab[j] = j * P for j = 0..8 (tab[0] = identity)
 __device__ __forceinline__ void build_table(const LaneTable& tab, const ge_p3& P) {
   ge_cached p1 = ge_p3_to_cached(P);
@@ -484,6 +522,25 @@ __device__ __forceinline__ Digits24 recode24(const u32 x[5]) {
   }
   return r;
 }
+// Digit strings parked in LDS for the ladder (k_verify's 256-thread blocks), so no VGPR holds them
+// across the windows: per thread, word k at p[k * 256] (a wave's access is one conflict-free 256 B
+// row).  Words [0, 6): e_B's low-half radix-2^24 digits, [6, 11): its high half, [11, 16) and
+// [16, 21): the Digits16 strings of |c| and d (the uncached ladder).
+constexpr int BD_HI = B24_LO_DIGITS, BD_C = BD_HI + B24_HI_DIGITS, BD_D = BD_C + 5;
+constexpr int BASE_DIGIT_WORDS = BD_D + 5;   // 21 words per thread
+struct BaseDigits { i32* p; };
+__device__ __forceinline__ void park16(BaseDigits bd, int off, const Digits16& x) {
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) bd.p[(off + i) * 256] = (i32)x.w[i];
+}
+// digit of window w (w <= W - 2) of a parked Digits16 string: nibble w + 41 - W (recode16's layout)
+__device__ __forceinline__ i32 digit16(BaseDigits bd, int off, int w, int W) {
+  const int pos = w + 41 - W;
+  return (i32)(((u32)bd.p[(off + (pos >> 3)) * 256] >> (4 * (pos & 7))) & 15u) - 8;
+}
+__device__ __forceinline__ void base_digits_park(BaseDigits bd, const Digits24& el, const Digits24& eh) {
+  _Pragma("unroll") for (int i = 0; i < B24_LO_DIGITS; ++i) bd.p[i * 256] = el.d[i];
+  _Pragma("unroll") for (int i = 0; i < B24_HI_DIGITS; ++i) bd.p[(BD_HI + i) * 256] = eh.d[i + B24_LO_DIGITS - B24_HI_DIGITS];
+}
 __device__ __forceinline__ i32 next24(Digits24& x) {
   const i32 d = x.d[B24_LO_DIGITS - 1];
   _Pragma("unroll") for (int i = B24_LO_DIGITS - 1; i > 0; --i) x.d[i] = x.d[i - 1];
@@ -508,6 +565,13 @@ typedef __attribute__((address_space(3))) void nwc_lvoid;
 // profiles/r02/experiments.md), at the same occupancy (VGPR-bound to 2 waves per SIMD).
 #ifndef NWC_STAGE_ENTRIES
 #define NWC_STAGE_ENTRIES 1
+#endif
+// NWC_LADDER_PREFETCH: 1 = the ladder holds the next window's A/R entries in VGPRs through the
+// doublings (round 1-2 default); 0 = each entry is gathered coordinate by coordinate inside its
+// add (add_lt): no VGPR holds an entry across the doublings, the loop runs without spills, and
+// the sign of the digit is an address choice (+2.5 % verifies/s, profiles/r02/experiments.md).
+#ifndef NWC_LADDER_PREFETCH
+#define NWC_LADDER_PREFETCH 0
 #endif
 constexpr int STAGE_U4_PER_WAVE = NWC_STAGE_ENTRIES * 8 * 64;
 __device__ __forceinline__ void stage_fetch(uint4* stage, int e, const ge_niels_pad* src) {
@@ -554,17 +618,18 @@ __device__ __forceinline__ void ladder_dbl4(ge_p1p1& t) {
 
 // Basepoint digits of window w: settle pending loads, then DMA the entries into the wave's stage.
 // Returns the number of entries fetched (0, 1 or 2).
-__device__ __forceinline__ int base_fetch(int w, Digits24& el, Digits24& eh, i32& d0, i32& d1,
+__device__ __forceinline__ int base_fetch(int w, BaseDigits bd, i32& d0, i32& d1,
                                           const ge_niels_pad* T24, uint4* stage) {
   const int nb = base_window_digits(w);
   if (nb) {
-    d0 = next24(el);
+    const int i = w / 6;
+    d0 = bd.p[i * 256];
     // settle the A/R entry loads first (they landed during the doublings), so no wait placed
     // for them below also has to wait for the DMA
     stage_wait();
     stage_fetch(stage, 0, T24 + (d0 < 0 ? -d0 : d0));
     if (nb == 2) {
-      d1 = next24(eh);
+      d1 = bd.p[(BD_HI + i) * 256];
       if (NWC_STAGE_ENTRIES == 2) stage_fetch(stage, 1, T24 + B24_ENTRIES + (d1 < 0 ? -d1 : d1));
     }
   }
@@ -589,20 +654,21 @@ __device__ __forceinline__ void base_adds(ge_p1p1& t, int nb, i32 d0, i32 d1, ui
 }
 
 __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const LaneTable& tr, Digits16 cd, Digits16 dd,
-                                                 Digits24 el, Digits24 eh, const ge_niels_pad* T24,
+                                                 BaseDigits bd, const ge_niels_pad* T24,
                                                  uint4* stage, int W) {
   // Code-size discipline: the window body holds ONE doubling and ONE Niels add (rolled loops) and
   // two cached adds, so the hot loop stays inside the instruction cache.
   // A/R entries for the current window are loaded at the end of the previous window, so their
   // latency hides behind this window's doublings and only 80 registers are in flight.
   i32 da = cd.top, dr = dd.top;   // top digits are >= 0
+#if NWC_LADDER_PREFETCH
   ge_cached ea = ta.load(da), er = tr.load(dr);
   ge_p1p1 t = ge_cached_to_p1p1(ea);
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     if (w != W - 1) ladder_dbl4(t);
     i32 d0 = 0, d1 = 0;
-    const int nb = base_fetch(w, el, eh, d0, d1, T24, stage);
+    const int nb = base_fetch(w, bd, d0, d1, T24, stage);
     // two explicit adds (a rolled 2-iteration loop needs a selected copy of the entry: 40 more
     // live VGPRs, which spilled)
     if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(ea, da < 0));
@@ -615,6 +681,26 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
       er = tr.load(dr < 0 ? -dr : dr);
     }
   }
+#else
+  // no entry held across the doublings: each is gathered inside its add; the digit strings are
+  // parked in LDS (BaseDigits), so the loop carries only the accumulator and a few scalars
+  park16(bd, BD_C, cd);
+  park16(bd, BD_D, dd);
+  ge_p1p1 t = ge_cached_to_p1p1(ta.load(da));
+#pragma unroll 1
+  for (int w = W - 1; w >= 0; --w) {
+    if (w != W - 1) {
+      ladder_dbl4(t);
+      da = digit16(bd, BD_C, w, W);
+      t = add_lt(t, ta, da < 0 ? -da : da, da < 0);
+      dr = digit16(bd, BD_D, w, W);
+    }
+    i32 d0 = 0, d1 = 0;
+    const int nb = base_fetch(w, bd, d0, d1, T24, stage);
+    t = add_lt(t, tr, dr < 0 ? -dr : dr, dr < 0);
+    base_adds(t, nb, d0, d1, stage, T24);
+  }
+#endif
   return ge_p1p1_to_p2(t);
 }
 
@@ -622,7 +708,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
 // radix-256 Niels table (one add at every even window, no per-equation table or decompression).
 // ca: radix-256 digits of |c| starting at window (W-1) & ~1; c_neg flips every A entry.
 __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Digits16 dd, Digits256 ca, bool c_neg,
-                                                        const ge_niels* key_tab, Digits24 el, Digits24 eh,
+                                                        const ge_niels* key_tab, BaseDigits bd,
                                                         const ge_niels_pad* T24, uint4* stage, int W) {
   i32 dr = dd.top;   // >= 0
   ge_cached er = tr.load(dr);
@@ -633,7 +719,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Dig
   for (int w = W - 1; w >= 0; --w) {
     if (w != W - 1) ladder_dbl4(t);
     i32 d0 = 0, d1 = 0;
-    const int nb = base_fetch(w, el, eh, d0, d1, T24, stage);
+    const int nb = base_fetch(w, bd, d0, d1, T24, stage);
     if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
     if ((w & 1) == 0) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(ean, (dA < 0) != c_neg));
     base_adds(t, nb, d0, d1, stage, T24);
@@ -751,8 +837,8 @@ __device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digi
 // from the cache: no decompression of A, no per-equation A table, 18 Niels adds for the A term.
 template <bool CACHE>
 __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels_pad* T24,
-                            uint4* stage, const LaneTable& ta, const LaneTable& tr, const Committee& cm,
-                            bool& fallback) {
+                            uint4* stage, BaseDigits bd, const LaneTable& ta, const LaneTable& tr,
+                            const Committee& cm, bool& fallback) {
   const int key = CACHE ? committee_lookup(cm, aw) : -1;
   if (CACHE && __all(key >= 0)) {
     u32 rw[8], sw[8];
@@ -771,12 +857,15 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
     // odd W: the top radix-256 digit of |c| (window W-1) is then < 2^3 + 1, never 128
     const int W = wave_windows(h.ok ? h.bits : 0) | 1;
     fallback = !h.ok;
-    Digits24 el, eh;
-    base_digits(h.d, sw, el, eh);
+    {
+      Digits24 el, eh;
+      base_digits(h.d, sw, el, eh);
+      base_digits_park(bd, el, eh);
+    }
     const Digits16 dd = recode16(h.d, W);
     const Digits256 ca = recode256(h.c, ((W - 1) >> 1) + 1);
     build_table(tr, ge_p3_neg(R[0]));
-    const ge_p2 q = half_scalarmult_cached(tr, dd, ca, h.c_neg, cm.tables + (size_t)key * 129, el, eh, T24, stage, W);
+    const ge_p2 q = half_scalarmult_cached(tr, dd, ca, h.c_neg, cm.tables + (size_t)key * 129, bd, T24, stage, W);
     const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
     return ok && ident && h.ok;
   }
@@ -785,13 +874,16 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
   const lat::HalfScalars h = lat::reduce(p.kw);
   const int W = wave_windows(h.ok ? h.bits : 0);
   fallback = !h.ok;
-  Digits24 el, eh;
-  base_digits(h.d, p.sw, el, eh);
+  {
+    Digits24 el, eh;
+    base_digits(h.d, p.sw, el, eh);
+    base_digits_park(bd, el, eh);
+  }
   const Digits16 cd = recode16(h.c, W), dd = recode16(h.d, W);
   // -c A = |c| * (c < 0 ? A : -A);  -d R = d * (-R)
   build_table(ta, h.c_neg ? p.A : ge_p3_neg(p.A));
   build_table(tr, ge_p3_neg(p.R));
-  const ge_p2 q = half_scalarmult(ta, tr, cd, dd, el, eh, T24, stage, W);
+  const ge_p2 q = half_scalarmult(ta, tr, cd, dd, bd, T24, stage, W);
   const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
   return p.ok && ident && h.ok;
 }
@@ -854,10 +946,11 @@ template <bool HALF, bool CACHE, bool LIST = false>
 __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(VerifyArgs a, CombArgs ca) {
   // HALF: per-wave LDS-DMA staging of radix-2^24 basepoint entries (8 KB per wave);
   // full-length ladder: the radix-256 basepoint table (15.5 KB).
-  __shared__ uint4 lds[HALF ? 4 * STAGE_U4_PER_WAVE : 129 * 30 / 4];
+  __shared__ uint4 lds[HALF ? 4 * STAGE_U4_PER_WAVE + BASE_DIGIT_WORDS * 64 : 129 * 30 / 4];
   ge_niels* sB = reinterpret_cast<ge_niels*>(lds);
   if constexpr (!HALF) stage_base_tables(a.base_table, sB, 129);
-  uint4* stage = lds + (threadIdx.x >> 6) * STAGE_U4_PER_WAVE;
+  uint4* stage = lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * STAGE_U4_PER_WAVE;
+  const BaseDigits bd{reinterpret_cast<i32*>(lds + 4 * STAGE_U4_PER_WAVE) + threadIdx.x};
   const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t* base = a.scratch + slot * 2 * TAB_BYTES_PER_LANE;
   const LaneTable ta{reinterpret_cast<uint4*>(base)};
@@ -872,7 +965,7 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
     load_inputs(a, active ? i : 0, mw, aw, sgw);
     bool fb = false;
     bool v;
-    if constexpr (HALF) v = verify_half<CACHE>(mw, aw, sgw, a.strict != 0, a.base24, stage, ta, tr, a.committee, fb);
+    if constexpr (HALF) v = verify_half<CACHE>(mw, aw, sgw, a.strict != 0, a.base24, stage, bd, ta, tr, a.committee, fb);
     else v = verify_full(mw, aw, sgw, a.strict != 0, sB, ta);
     if (HALF && a.force_fb_every && (i % a.force_fb_every) == 0) { fb = true; v = false; }
     v = v && active;

@@ -239,6 +239,7 @@ int init_device(DevCtx& d) {
   int bpc = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify<true, false>), 256, 0));
   d.verify_blocks_per_cu = bpc > 0 ? bpc : 1;
+  if (std::getenv("NWC_SHOW_OCCUPANCY")) std::fprintf(stderr, "nwc: k_verify resident blocks per CU %d\n", bpc);
   bpc = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify_comb), 256, 0));
   d.comb_blocks_per_cu = bpc > 0 ? bpc : 1;
