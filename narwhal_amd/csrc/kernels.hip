@@ -838,7 +838,7 @@ __device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digi
 template <bool CACHE>
 __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], const u32 sigw[16], bool strict, const ge_niels_pad* T24,
                             uint4* stage, BaseDigits bd, const LaneTable& ta, const LaneTable& tr,
-                            const Committee& cm, bool& fallback) {
+                            const Committee& cm, bool& fallback, int force_w) {
   const int key = CACHE ? committee_lookup(cm, aw) : -1;
   if (CACHE && __all(key >= 0)) {
     u32 rw[8], sw[8];
@@ -855,7 +855,7 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
     challenge(rw, aw, mw, kw);
     const lat::HalfScalars h = lat::reduce(kw);
     // odd W: the top radix-256 digit of |c| (window W-1) is then < 2^3 + 1, never 128
-    const int W = wave_windows(h.ok ? h.bits : 0) | 1;
+    const int W = max(wave_windows(h.ok ? h.bits : 0), min(force_w, HALF_WINDOWS_MAX)) | 1;
     fallback = !h.ok;
     {
       Digits24 el, eh;
@@ -872,7 +872,7 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
   Prologue p;
   prologue<1>(p, mw, aw, sigw, strict);
   const lat::HalfScalars h = lat::reduce(p.kw);
-  const int W = wave_windows(h.ok ? h.bits : 0);
+  const int W = max(wave_windows(h.ok ? h.bits : 0), min(force_w, HALF_WINDOWS_MAX));
   fallback = !h.ok;
   {
     Digits24 el, eh;
@@ -911,6 +911,7 @@ struct VerifyArgs {
   uint32_t* fb_count;
   uint32_t force_fb_every;      // test hook: route equations i % every == 0 to the fallback (0 = off)
   Committee committee;          // n == 0: no cache
+  uint32_t force_windows;       // test hook: run the half-size ladder with at least this many windows (0 = off)
 };
 // Extra arguments of the comb path (kept out of VerifyArgs so the headline kernel's argument
 // block and register allocation do not change).
@@ -965,7 +966,8 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
     load_inputs(a, active ? i : 0, mw, aw, sgw);
     bool fb = false;
     bool v;
-    if constexpr (HALF) v = verify_half<CACHE>(mw, aw, sgw, a.strict != 0, a.base24, stage, bd, ta, tr, a.committee, fb);
+    if constexpr (HALF) v = verify_half<CACHE>(mw, aw, sgw, a.strict != 0, a.base24, stage, bd, ta, tr, a.committee, fb,
+                                                 (int)a.force_windows);
     else v = verify_full(mw, aw, sgw, a.strict != 0, sB, ta);
     if (HALF && a.force_fb_every && (i % a.force_fb_every) == 0) { fb = true; v = false; }
     v = v && active;

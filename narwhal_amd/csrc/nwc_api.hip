@@ -518,6 +518,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
   nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
+  if (const char* e = std::getenv("NWC_FORCE_WINDOWS")) a.force_windows = (uint32_t)std::strtoul(e, nullptr, 10);
   const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
   const bool half = path != VPath::Full;
   // small batch-leaf launches outside the comb path: the keys' torsion test (one long serial
