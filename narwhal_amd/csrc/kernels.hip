@@ -658,8 +658,8 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
                                                  uint4* stage, int W) {
   // Code-size discipline: the window body holds ONE doubling and ONE Niels add (rolled loops) and
   // two cached adds, so the hot loop stays inside the instruction cache.
-  // A/R entries for the current window are loaded at the end of the previous window, so their
-  // latency hides behind this window's doublings and only 80 registers are in flight.
+  // NWC_LADDER_PREFETCH=1 (round 1-2): the A/R entries of the next window are loaded at the end of
+  // the previous one, so their latency hides behind the doublings (80 VGPRs held through them).
   i32 da = cd.top, dr = dd.top;   // top digits are >= 0
 #if NWC_LADDER_PREFETCH
   ge_cached ea = ta.load(da), er = tr.load(dr);
