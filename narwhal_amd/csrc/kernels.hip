@@ -29,6 +29,18 @@
 #include "lattice.h"
 #include "fe_sliced.h"
 
+// Build switches of the half-size ladder (A/B experiments, profiles/r02/experiments.md):
+//   NWC_BASE_FETCH_EARLY  issue a window's first basepoint DMA before its doublings (1) or after
+//                         the A add (0)
+//   NWC_ADD_LT_SPLIT      add_lt gathers Z and 2dT only after the extended form is built (1) or
+//                         all four coordinates up front (0)
+#ifndef NWC_BASE_FETCH_EARLY
+#define NWC_BASE_FETCH_EARLY 1
+#endif
+#ifndef NWC_ADD_LT_SPLIT
+#define NWC_ADD_LT_SPLIT 1
+#endif
+
 namespace nwc {
 
 // ------------------------------------------------------------------------------- helpers
@@ -347,7 +359,9 @@ __device__ __forceinline__ ge_p1p1 add_lt(const ge_p1p1& t, const LaneTable& tab
   const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Y, t.Z);
   const fe a = fe_add(Y3, X3), b = fe_sub(Y3, X3);
   const fe Z3 = fe_mul(t.Z, t.T), T3 = fe_mul(t.X, t.Y);
+#if NWC_ADD_LT_SPLIT
   __builtin_amdgcn_sched_barrier(0);
+#endif
   const fe qz = lt_load_fe(tab, e, 2);
   const fe qt = lt_load_fe(tab, e, 3);
   const fe pp = fe_mul(a, qa), mm = fe_mul(b, qb);
@@ -689,14 +703,21 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
   ge_p1p1 t = ge_cached_to_p1p1(ta.load(da));
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
+    i32 d0 = 0, d1 = 0;
+#if NWC_BASE_FETCH_EARLY
+    // the window's first basepoint entry lands during the doublings; the A/R gathers issued
+    // after it then never wait on the DMA (vmcnt counts in order)
+    const int nb = base_fetch(w, bd, d0, d1, T24, stage);
+#endif
     if (w != W - 1) {
       ladder_dbl4(t);
       da = digit16(bd, BD_C, w, W);
       t = add_lt(t, ta, da < 0 ? -da : da, da < 0);
       dr = digit16(bd, BD_D, w, W);
     }
-    i32 d0 = 0, d1 = 0;
+#if !NWC_BASE_FETCH_EARLY
     const int nb = base_fetch(w, bd, d0, d1, T24, stage);
+#endif
     t = add_lt(t, tr, dr < 0 ? -dr : dr, dr < 0);
     base_adds(t, nb, d0, d1, stage, T24);
   }
