@@ -104,6 +104,10 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;      // small batch-leaf calls: the keys' torsion test beside the verification
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // large host calls: input chunks are copied on `xfer` while the previous chunk verifies on
+  // `stream` (one event per chunk in flight, created on first use)
+  hipStream_t xfer = nullptr;
+  std::vector<hipEvent_t> ev_chunk;
   nwc::ge_niels* base_table = nullptr;
   nwc::ge_niels_pad* base24 = nullptr;   // radix-2^24 basepoint tables (2.1 GB)
   nwc::ge_p3* base24_points = nullptr;    // B and 2^141 B
@@ -191,6 +195,11 @@ struct DevCtx {
 #endif
 
 // batches up to this size take the latency kernel (k_verify_comb_wide) on the comb path
+// Host calls of at least 2 chunks are pipelined: chunk i+1's inputs cross PCIe while chunk i
+// verifies.  A chunk is one full round of resident lanes (2 blocks of 256 per CU x 256 CUs).
+#ifndef NWC_HOST_CHUNK
+#define NWC_HOST_CHUNK (1u << 17)
+#endif
 #ifndef NWC_PINNED_STAGE_MAX
 #define NWC_PINNED_STAGE_MAX (1u << 20)
 #endif
@@ -733,6 +742,41 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
       if (int rc = auto_insert(d, pks + 32 * lo, n)) return rc;
     return 0;
   }
+  static const uint64_t chunk = [] {
+    const char* e = std::getenv("NWC_HOST_CHUNK");   // 0 = no pipelining (A/B)
+    return e ? (uint64_t)std::strtoull(e, nullptr, 10) / 64 * 64 : (uint64_t)NWC_HOST_CHUNK;
+  }();
+  if (chunk && n >= 2 * chunk) {
+    // pipelined: inputs of chunk k on the transfer stream, its verification on the device stream
+    // after the chunk's event; every chunk has its own region of the arena (no reuse hazards)
+    if (!d.xfer) HIP_TRY(hipStreamCreateWithFlags(&d.xfer, hipStreamNonBlocking));
+    const uint64_t nch = (n + chunk - 1) / chunk;
+    while (d.ev_chunk.size() < nch) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      d.ev_chunk.push_back(e);
+    }
+    // the previous call's kernels may still read the arena: the transfers wait for the stream
+    HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
+    HIP_TRY(hipStreamWaitEvent(d.xfer, d.ev_fork, 0));
+    if (msg_index) HIP_TRY(hipMemcpyAsync(dm, msgs, msg_bytes, hipMemcpyHostToDevice, d.xfer));
+    else if (!msg_stride) HIP_TRY(hipMemcpyAsync(dm, msgs, 32, hipMemcpyHostToDevice, d.xfer));
+    for (uint64_t k = 0; k < nch; ++k) {
+      const uint64_t c0 = k * chunk, len = std::min<uint64_t>(chunk, n - c0);
+      if (msg_index) HIP_TRY(hipMemcpyAsync(dmi + c0, msg_index + lo + c0, 4 * len, hipMemcpyHostToDevice, d.xfer));
+      else if (msg_stride) HIP_TRY(hipMemcpyAsync(dm + 32 * c0, msgs + 32 * (lo + c0), 32 * len, hipMemcpyHostToDevice, d.xfer));
+      HIP_TRY(hipMemcpyAsync(dp + 32 * c0, pks + 32 * (lo + c0), 32 * len, hipMemcpyHostToDevice, d.xfer));
+      HIP_TRY(hipMemcpyAsync(ds + 64 * c0, sigs + 64 * (lo + c0), 64 * len, hipMemcpyHostToDevice, d.xfer));
+      HIP_TRY(hipEventRecord(d.ev_chunk[k], d.xfer));
+      HIP_TRY(hipStreamWaitEvent(d.stream, d.ev_chunk[k], 0));
+      if (int rc = launch_verify(d, msg_stride ? dm + 32 * c0 : dm, msg_index ? dmi + c0 : nullptr, msg_stride ? 1 : 0,
+                                 dp + 32 * c0, ds + 64 * c0, len, strict, dout + c0 / 64, d.stream))
+        return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(out_words.data(), dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    return 0;
+  }
   if (msg_index) {
     HIP_TRY(hipMemcpyAsync(dm, msgs, msg_bytes, hipMemcpyHostToDevice, d.stream));
     HIP_TRY(hipMemcpyAsync(dmi, msg_index + lo, 4 * n, hipMemcpyHostToDevice, d.stream));
@@ -851,6 +895,9 @@ void nwc_shutdown(void) {
     if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
     if (d->ev_join) (void)hipEventDestroy(d->ev_join);
     if (d->side) (void)hipStreamDestroy(d->side);
+    if (d->xfer) (void)hipStreamSynchronize(d->xfer);
+    for (hipEvent_t e : d->ev_chunk) (void)hipEventDestroy(e);
+    if (d->xfer) (void)hipStreamDestroy(d->xfer);
     if (d->stream) (void)hipStreamDestroy(d->stream);
   }
   g_devs.clear();

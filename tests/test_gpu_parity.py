@@ -345,3 +345,35 @@ def test_full_size_1m_all_valid_and_exact_failures(lib, oracle, torch_dev):
     assert list(np.nonzero(~got)[0]) == list(idx)
     sub = [t[ti].cpu().numpy() for t in (msgs, pks, sigs)]
     assert not oracle.strict_many(*sub).any()
+
+
+def test_host_calls_pipelined_chunks_vs_oracle(lib, oracle, torch_dev):
+    """Host-memory calls of 2+ chunks (NWC_HOST_CHUNK = 131,072 equations) copy chunk k+1 while
+    chunk k verifies: strict triples (per-triple digests) and certificates (msg_index into the
+    digests; a certificate may straddle a chunk cut) with corrupted entries, against the oracle."""
+    torch = torch_dev
+    from narwhal_amd import _lib, device
+    n = 2 * 131072 + 12345
+    msgs, pks, sigs = _random_triples(torch, device, n, tag=b"chunks")
+    m, p, s = (t.cpu().numpy().copy() for t in (msgs, pks, sigs))
+    rng = np.random.default_rng(21)
+    bad = np.sort(rng.choice(n, 997, replace=False))
+    s[bad[::2], 40] ^= 4
+    m[bad[1::2], 7] ^= 1
+    got = _strict_many(lib, m, p, s)
+    assert (got == oracle.strict_many(m, p, s)).all()
+    assert list(np.nonzero(~got)[0]) == list(bad)
+    # certificates of 67 votes over one digest each, the votes signed by device keys
+    Q, mc = 67, n // 67
+    digests = rng.integers(0, 256, (mc, 32), dtype=np.uint8)
+    vm = torch.from_numpy(np.repeat(digests, Q, axis=0)).cuda()
+    pk2, sg2 = device.keygen_sign(device.derive32(b"chunks-seed", 0, mc * Q), vm)
+    p2, s2 = pk2.cpu().numpy().copy(), sg2.cpu().numpy().copy()
+    s2[rng.choice(mc * Q, 500, replace=False), 33] ^= 1
+    offs = (np.arange(mc + 1) * Q).astype(np.uint32)
+    cert = ctypes.create_string_buffer((mc + 7) // 8)
+    badb = ctypes.create_string_buffer((mc * Q + 7) // 8)
+    _lib.check(lib.nwc_verify_batch_many(_lib.buf(digests), _lib.buf(offs), _lib.buf(p2), _lib.buf(s2), mc, cert, badb))
+    ocert, obad = oracle.batch_many(digests, offs, p2, s2)
+    assert (_bits(cert.raw, mc) == ocert).all()
+    assert (_bits(badb.raw, mc * Q) == obad).all()
