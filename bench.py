@@ -674,6 +674,31 @@ def roofline_verify(vpc, n: int, kernel_ms: float, effective_tops: float):
 
 
 # ---- main ------------------------------------------------------------------------------------
+def bench_cfg2_host_abi(lib, msgs, pks, sigs, reps: int):
+    """Config 2 end to end ("plus a separate end-to-end time"): the same triples
+    from pageable host memory through nwc_verify_strict_many (PCIe in, chunk-pipelined, verdict
+    bitmap out); never the headline value."""
+    import ctypes
+    import numpy as np
+    from narwhal_amd import _lib
+    m, p, s = (np.ascontiguousarray(t.cpu().numpy()) for t in (msgs, pks, sigs))
+    n = p.shape[0]
+    out = ctypes.create_string_buffer((n + 7) // 8)
+    vp = ctypes.c_void_p
+    call = lambda: lib.nwc_verify_strict_many(m.ctypes.data_as(vp), p.ctypes.data_as(vp), s.ctypes.data_as(vp),  # noqa: E731
+                                              ctypes.c_size_t(n), out)
+    _lib.check(call())
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _lib.check(call())
+        ts.append(time.perf_counter() - t0)
+    med = sorted(ts)[len(ts) // 2]
+    ok = bool(np.unpackbits(np.frombuffer(out.raw, np.uint8), bitorder="little")[:n].all())
+    return {"workload": "cfg2 triples from pageable host buffers, nwc_verify_strict_many (H2D + verify + D2H)",
+            "verifies_per_s": n / med, "ms_per_call": med * 1e3, "reps": reps, "verdicts_ok": ok}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -689,6 +714,8 @@ def main():
     ap.add_argument("--cfg1-calls", type=int, default=10000, help="config 1 latency calls (0 = skip)")
     ap.add_argument("--wire-certs", type=int, default=20000, help="cfg 3 from wire bytes (0 = skip)")
     ap.add_argument("--cfg5-total", type=int, default=64 << 20, help="cfg 5 signatures over all ranks (0 = skip)")
+    ap.add_argument("--e2e-reps", type=int, default=3,
+                    help="cfg 2 end to end through the host ABI from pageable host buffers (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -767,6 +794,8 @@ def main():
                   "effective_valu_frac": dk_gbs * 1e9 / 128 * OPS_SHA / (VALU_PEAK_TOPS * 1e12)}
 
     extras = {}
+    if world == 1 and args.e2e_reps > 0:
+        extras["cfg2_host_abi"] = bench_cfg2_host_abi(lib, msgs, pks, sigs, args.e2e_reps)
     if args.cfg5_total > 0:
         extras["cfg5"] = bench_cfg5(lib, rank, world, args.cfg5_total, 2)
     if world == 1 and args.cfg3_certs > 0:

@@ -6,7 +6,7 @@ set -e
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 ROUNDS=$1; shift
 mkdir -p $R/gpurun_out
-ARGS="--steps 10 --warmup 2 --cpu-budget 0 --cfg1-calls 0 --cfg3-certs 0 --wire-certs 0 --cfg5-total 0 --digest-batches 0 ${AB_ARGS:-}"
+ARGS="--steps 10 --warmup 2 --cpu-budget 0 --cfg1-calls 0 --cfg3-certs 0 --wire-certs 0 --cfg5-total 0 --e2e-reps 0 --digest-batches 0 ${AB_ARGS:-}"
 for r in $(seq 1 $ROUNDS); do
   for lib in "$@"; do
     NWC_LIB_PATH=$R/$lib timeout -k 10 180 python3 $R/bench.py $ARGS > $R/gpurun_out/ab_last.json 2> $R/gpurun_out/ab_last.err

@@ -6,7 +6,7 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --cpu-budget 0 --cfg1-calls 0 --cfg3-certs 0 --wire-certs 0 --cfg5-total 0 --digest-batches 0"
+ARGS="--steps 2 --warmup 1 --cpu-budget 0 --cfg1-calls 0 --cfg3-certs 0 --wire-certs 0 --cfg5-total 0 --e2e-reps 0 --digest-batches 0"
 SETS=${PMC_SETS:-"SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE;SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM SQ_INSTS_LDS;SQ_WAVES FETCH_SIZE;SQ_WAVES WRITE_SIZE"}
 IFS=';' read -ra SETARR <<< "$SETS"
 for lib in "$@"; do
