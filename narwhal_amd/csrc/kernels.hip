@@ -1420,8 +1420,11 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
     const bool flags_ok = key >= 0 && sc_lt_l(sw) && key_flags_ok(fl, a.strict != 0) && sh_rok;
     const bool eq = fe_is_zero(fe_sub(sum.X, fe_mul(sh_rx, sum.Z))) && fe_is_zero(fe_sub(sum.Y, fe_mul(sh_ry, sum.Z)));
     if (ca.vbytes) {
-      // zero-copy latency launch: one byte per equation straight into pinned host memory
-      ca.vbytes[i] = (uint8_t)((flags_ok && eq ? 1u : 0u) | (key < 0 ? 2u : 0u));
+      // zero-copy latency launch: one byte per equation straight into pinned host memory; bit 7
+      // marks it written, and the system-scope store goes out at once, so the host can return as
+      // soon as every byte is in (no wait for the stream's completion signal)
+      __hip_atomic_store(ca.vbytes + i, (uint8_t)(0x80u | (flags_ok && eq ? 1u : 0u) | (key < 0 ? 2u : 0u)),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     } else {
       if (key < 0) {
         if (ca.list) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;

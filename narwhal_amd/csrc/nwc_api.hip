@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -168,7 +169,8 @@ struct DevCtx {
   int ensure_pinned(size_t bytes) {
     if (bytes <= pinned_cap) return 0;
     if (pinned) { (void)hipHostFree(pinned); pinned = nullptr; pinned_cap = 0; }
-    HIP_TRY(hipHostMalloc(&pinned, bytes, hipHostMallocDefault));
+    // coherent: the latency kernel's verdict bytes reach the host while it polls them
+    HIP_TRY(hipHostMalloc(&pinned, bytes, hipHostMallocCoherent));
     void* dp = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dp, pinned, 0));
     pinned_dev = static_cast<uint8_t*>(dp);
@@ -712,7 +714,31 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
       if (int rc = launch_verify(d, dev(dm), reinterpret_cast<const uint32_t*>(dev(dmi)), msg_stride ? 1 : 0, dev(dp),
                                  dev(ds), n, strict, dout, d.stream, fl, d.pinned_dev + (hb - h)))
         return rc;
-      HIP_TRY(hipStreamSynchronize(d.stream));
+      static const bool spin = [] {
+        const char* e = std::getenv("NWC_SPIN_WAIT");   // 0 = wait for the stream (A/B)
+        return !(e && std::strcmp(e, "0") == 0);
+      }();
+      if (spin) {
+        // poll the verdict bytes (bit 7 = written); a launch that never writes them (a device
+        // error) falls back to the stream wait after 200 ms, which reports the error
+        const volatile uint8_t* vb = hb;
+        const auto t0 = std::chrono::steady_clock::now();
+        uint64_t done = 0;
+        for (;;) {
+          while (done < n && (vb[done] & 0x80u)) ++done;
+          if (done == n) break;
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+            HIP_TRY(hipStreamSynchronize(d.stream));
+            for (done = 0; done < n && (vb[done] & 0x80u); ++done) {}
+            if (done != n) return set_err(NWC_ERR_DEVICE, "latency kernel left verdicts unwritten");
+            break;
+          }
+          __builtin_ia32_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+      } else {
+        HIP_TRY(hipStreamSynchronize(d.stream));
+      }
       bool missing = false;
       for (uint64_t i = 0; i < n; ++i) {
         if (hb[i] & 1) out_words[i >> 6] |= 1ull << (i & 63);

@@ -33,6 +33,6 @@ for i in range(n_calls + 100):
     if i >= 100:
         lat[i - 100] = dt * 1e6
 q = np.percentile(lat, [50, 90, 99, 99.9])
-print(json.dumps({"zero_copy": os.environ.get("NWC_ZERO_COPY", "1"), "calls": n_calls,
+print(json.dumps({"zero_copy": os.environ.get("NWC_ZERO_COPY", "1"), "spin_wait": os.environ.get("NWC_SPIN_WAIT", "1"), "calls": n_calls,
                   "p50_us": q[0], "p90_us": q[1], "p99_us": q[2], "p999_us": q[3], "max_us": float(lat.max()),
                   "over_100us": int((lat > 100).sum())}))
