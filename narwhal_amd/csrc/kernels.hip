@@ -246,11 +246,13 @@ __global__ void k_build_key_tables(const u32* __restrict__ keys, u32 n, ge_niels
 // (affine Niels, 128-B entries) so that x * P = sum_w comb[w][d_w] (a negative digit negates the
 // entry) for the signed radix-2^BITS digits d_w of any x < 2^253.
 //   BaseComb: P = B, radix 2^8, 32 windows (528 KB, nwc_init) -- the latency kernel's basepoint
-//   KeyComb:  P = -A_key, radix 2^12, 22 windows (5.8 MB per key, nwc_set_committee)
+//   KeyComb:  P = -A_key, radix 2^14, 19 windows (20 MB per key, nwc_set_committee / auto cache)
 // One lane per entry: BITS*w doublings of P, a BITS-bit double-and-add, one inversion.
+// Radix measured on config 3 with the committee cached (tools/ab_cfg3.sh, profiles/r02/experiments.md):
+// key combs 2^12 / 2^14 / 2^16 with a 2^22 basepoint comb: 583-593 / 615 / 528-533 M votes/s.
 #ifndef NWC_KEY_COMB_BITS
-#define NWC_KEY_COMB_BITS 12
-#define NWC_KEY_COMB_WINDOWS 22
+#define NWC_KEY_COMB_BITS 14
+#define NWC_KEY_COMB_WINDOWS 19
 #endif
 template <int BITS, int WINDOWS>
 struct CombShape {
@@ -290,21 +292,37 @@ __global__ void k_build_comb(const u32* __restrict__ keys, u32 n, ge_niels_pad* 
   out[t].pad[1] = 0;
 }
 
-// Radix-2^16 basepoint comb for the throughput committee kernel: comb16[w * 32769 + j] =
-// j * 2^(16 w) * B, w = 0..15, j = 0..32768 (67 MB, MALL-resident next to the key combs): s*B is
-// 16 additions instead of 32.  One lane per entry (16w doublings, a 16-bit double-and-add, one
-// inversion), built once at nwc_init.
-constexpr int COMB16_WINDOWS = 16, COMB16_ENTRIES = 32769;
-constexpr size_t COMB16_TOTAL = (size_t)COMB16_WINDOWS * COMB16_ENTRIES;
-__global__ void k_build_comb16(ge_niels_pad* __restrict__ out) {
+// Basepoint comb for the throughput committee kernel: comb16[w * E + j] = j * 2^(BITS w) * B,
+// w < WINDOWS, j = 0..2^(BITS-1) (E entries per window; radix 2^22: 12 x 2,097,153 entries =
+// 3.2 GB of the 288 GB HBM): s*B is 12 additions instead of 16 at radix 2^16 (67 MB; 541 -> 590 M
+// votes/s on config 3, profiles/r02/experiments.md; 2^24 / 11 windows / 11.8 GB gained nothing
+// more).  Built once at nwc_init (~60 ms): k_bcomb_bases doubles B into the window bases on one
+// lane, then one lane per entry runs a BITS-bit double-and-add and one inversion.
+#ifndef NWC_BCOMB_BITS
+#define NWC_BCOMB_BITS 22
+#endif
+#ifndef NWC_BCOMB_WINDOWS
+#define NWC_BCOMB_WINDOWS 12
+#endif
+using BCombShape = CombShape<NWC_BCOMB_BITS, NWC_BCOMB_WINDOWS>;
+constexpr int COMB16_WINDOWS = BCombShape::windows, COMB16_ENTRIES = BCombShape::entries;
+constexpr size_t COMB16_TOTAL = BCombShape::per;
+__global__ void k_bcomb_bases(ge_p3* out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  ge_p3 b = ge_base_point();
+  for (int w = 0; w < COMB16_WINDOWS; ++w) {
+    out[w] = b;
+    for (int k = 0; k < NWC_BCOMB_BITS; ++k) b = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(b)));
+  }
+}
+__global__ void k_build_comb16(ge_niels_pad* __restrict__ out, const ge_p3* __restrict__ bases) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= COMB16_TOTAL) return;
   const int w = (int)(t / COMB16_ENTRIES), j = (int)(t % COMB16_ENTRIES);
-  ge_p3 P = ge_base_point();
-  for (int k = 0; k < 16 * w; ++k) P = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
-  const ge_cached pc = ge_p3_to_cached(P);
+  const ge_cached pc = ge_p3_to_cached(bases[w]);
   ge_p3 acc = ge_p3_identity();
-  for (int bit = 15; bit >= 0; --bit) {
+#pragma unroll 1
+  for (int bit = NWC_BCOMB_BITS - 1; bit >= 0; --bit) {
     acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
     if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, pc));
   }
@@ -1221,19 +1239,14 @@ __device__ __forceinline__ ge_p1p1 ge_niels_to_p1p1(const ge_niels& q) {
   return r;
 }
 
-// s B + k (-A) with the radix-2^16 basepoint comb (16 windows) and the key's radix-2^12 comb
-// (22 windows): 38 additions -- the key's windows 21..0, then B's 15..0.  Entry i+1 is fetched
+// s B + k (-A) with the basepoint comb (COMB16_WINDOWS windows of radix 2^NWC_BCOMB_BITS) and the
+// key's comb (radix 2^14, 19 windows): 31 additions by default -- the key's windows, then B's.  Entry i+1 is fetched
 // before entry i is added, so one fetch is in flight behind every addition.
-__device__ __forceinline__ i32 next_digit16(u32 d[8]) {
-  const i32 v = (i32)(d[7] >> 16) - 32768;
-  digits_shl(d, 16);
-  return v;
-}
-constexpr int COMB_SUM_ADDS = KeyComb::windows + COMB16_WINDOWS;   // 38 (radix 2^12)
+constexpr int COMB_SUM_ADDS = KeyComb::windows + COMB16_WINDOWS;   // 31 (19 key + 12 basepoint windows)
 __device__ __forceinline__ ge_p2 comb_sum(const u32 sw[8], const u32 kw[8], const ge_niels_pad* TB16,
                                           const ge_niels_pad* TA) {
-  u32 sd[8], kd[9];
-  sc_recode_radix65536(sw, sd);
+  u32 sd[9], kd[9];
+  sc_recode_radix<NWC_BCOMB_BITS, COMB16_WINDOWS>(sw, sd);
   sc_recode_radix<KeyComb::bits, KeyComb::windows>(kw, kd);
   i32 d = digit_at<KeyComb::bits>(kd, KeyComb::windows - 1);
   ge_niels e = comb_load(TA, KeyComb::entries, KeyComb::windows - 1, d);
@@ -1249,7 +1262,7 @@ __device__ __forceinline__ ge_p2 comb_sum(const u32 sw[8], const u32 kw[8], cons
       dn = digit_at<KeyComb::bits>(kd, KeyComb::windows - 1 - nx);
       en = comb_load(TA, KeyComb::entries, KeyComb::windows - 1 - nx, dn);
     } else if (nx < COMB_SUM_ADDS) {
-      dn = next_digit16(sd);
+      dn = digit_at<NWC_BCOMB_BITS>(sd, COMB_SUM_ADDS - 1 - nx);
       en = comb_load(TB16, COMB16_ENTRIES, COMB_SUM_ADDS - 1 - nx, dn);
     }
     t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(e, d < 0));
@@ -1393,7 +1406,7 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
       sh_rok = ok && !(a.strict && ycanon_is_small_order(yc));
     }
   } else {
-    // lanes 0..31: basepoint comb (radix 2^8) windows; lanes 32..53: key comb (radix 2^12)
+    // lanes 0..31: basepoint comb (radix 2^8) windows; lanes 32..32+W-1: key comb windows (W = 19)
     // windows; lanes 54..63 hold the identity
     key = committee_lookup(cm, aw);
     kk = key < 0 ? 0 : key;

@@ -113,7 +113,8 @@ struct DevCtx {
   nwc::ge_niels_pad* base24 = nullptr;   // radix-2^24 basepoint tables (2.1 GB)
   nwc::ge_p3* base24_points = nullptr;    // B and 2^141 B
   nwc::ge_niels_pad* comb_base = nullptr;   // radix-256 basepoint comb (528 KB): latency kernel
-  nwc::ge_niels_pad* comb16 = nullptr;      // radix-2^16 basepoint comb (67 MB): k_verify_comb
+  nwc::ge_niels_pad* comb16 = nullptr;      // basepoint comb (radix 2^NWC_BCOMB_BITS, 67 MB at 2^16): k_verify_comb
+  nwc::ge_p3* comb16_bases = nullptr;       // its window bases 2^(bits w) B (built at init)
   int comb_blocks_per_cu = 1;
   uint32_t* uc_list = nullptr;     // k_verify_comb: equations whose key is not cached
   uint32_t* uc_count = nullptr;
@@ -191,7 +192,7 @@ struct DevCtx {
 #ifndef NWC_MEMO_SLOTS
 #define NWC_MEMO_SLOTS (1u << 16)
 #endif
-// committees up to this size get per-key combs (5.8 MB each); larger ones use the cached ladder
+// committees up to this size get per-key combs (20 MB each at radix 2^14); larger ones use the cached ladder
 #ifndef NWC_COMB_MAX_KEYS
 #define NWC_COMB_MAX_KEYS 1024
 #endif
@@ -260,8 +261,11 @@ int init_device(DevCtx& d) {
                      (const nwc::u32*)nullptr, 1u, d.comb_base);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMalloc(&d.comb16, nwc::COMB16_TOTAL * sizeof(nwc::ge_niels_pad)));
+  HIP_TRY(hipMalloc(&d.comb16_bases, nwc::COMB16_WINDOWS * sizeof(nwc::ge_p3)));
+  hipLaunchKernelGGL(nwc::k_bcomb_bases, dim3(1), dim3(64), 0, d.stream, d.comb16_bases);
+  HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(nwc::k_build_comb16, dim3((unsigned)((nwc::COMB16_TOTAL + 255) / 256)), dim3(256), 0, d.stream,
-                     d.comb16);
+                     d.comb16, (const nwc::ge_p3*)d.comb16_bases);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMalloc(&d.base_table, 2 * 129 * sizeof(nwc::ge_niels)));
   HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
@@ -292,7 +296,7 @@ int require_init() {
   return 0;
 }
 
-// NWC_AUTO_KEYS: capacity of the per-device auto key cache (default 256 keys, 5.8 MB of combs
+// NWC_AUTO_KEYS: capacity of the per-device auto key cache (default 256 keys, 20 MB of combs
 // each, allocated on first use; 0 disables it).
 uint32_t auto_keys_cap() {
   static const uint32_t cap = [] {
@@ -900,6 +904,7 @@ void nwc_shutdown(void) {
     if (d->ak_slots) (void)hipFree(d->ak_slots);
     if (d->comb_base) (void)hipFree(d->comb_base);
     if (d->comb16) (void)hipFree(d->comb16);
+    if (d->comb16_bases) (void)hipFree(d->comb16_bases);
     if (d->pinned) (void)hipHostFree(d->pinned);
     if (d->cc_stakes) (void)hipFree(d->cc_stakes);
     if (d->cc_worker_off) (void)hipFree(d->cc_worker_off);
@@ -1075,7 +1080,7 @@ static int set_committee_locked(const uint8_t* pks, size_t n) {
                        d.cm_tables, d.cm_flags);
     HIP_TRY(hipGetLastError());
     if (n <= NWC_COMB_MAX_KEYS) {
-      // per-key combs for the doubling-free path (radix 2^12: 5.8 MB per key)
+      // per-key combs for the doubling-free path (radix 2^14: 20 MB per key)
       const size_t entries = n * nwc::COMB_PER_KEY;
       HIP_TRY(hipMalloc(&d.cm_comb, entries * sizeof(nwc::ge_niels_pad)));
       hipLaunchKernelGGL(nwc::k_build_comb<nwc::KeyComb>, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, d.stream,
