@@ -292,6 +292,46 @@ __global__ void k_build_comb(const u32* __restrict__ keys, u32 n, ge_niels_pad* 
   out[t].pad[1] = 0;
 }
 
+// Key combs in two passes (the same points as k_build_comb<S>, ~4x less work): one lane per key
+// decodes it and doubles -A into the window bases 2^(BITS w) (-A); then one lane per entry runs a
+// BITS-bit double-and-add from its window's base and one inversion.
+template <class S>
+__global__ void k_comb_key_bases(const u32* __restrict__ keys, u32 n, ge_p3* __restrict__ bases) {
+  const u32 key = blockIdx.x * blockDim.x + threadIdx.x;
+  if (key >= n) return;
+  u32 kw[8];
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) kw[i] = keys[8 * key + i];
+  u32 yc[1][8];
+  bool ok[1];
+  const u32* const wp[1] = {kw};
+  ge_p3 P;
+  ge_decompressN<1>(&P, wp, yc, ok);
+  P = ge_p3_neg(P);
+#pragma unroll 1
+  for (int w = 0; w < S::windows; ++w) {
+    bases[(size_t)key * S::windows + w] = P;
+#pragma unroll 1
+    for (int k = 0; k < S::bits; ++k) P = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
+  }
+}
+template <class S>
+__global__ void k_build_comb_from_bases(const ge_p3* __restrict__ bases, u32 n, ge_niels_pad* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n * S::per) return;
+  const u32 key = (u32)(t / S::per), r = (u32)(t % S::per);
+  const int w = (int)(r / S::entries), j = (int)(r % S::entries);
+  const ge_cached pc = ge_p3_to_cached(bases[(size_t)key * S::windows + w]);
+  ge_p3 acc = ge_p3_identity();
+#pragma unroll 1
+  for (int bit = S::bits - 1; bit >= 0; --bit) {
+    acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
+    if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, pc));
+  }
+  out[t].n = ge_p3_to_niels(acc);
+  out[t].pad[0] = 0;
+  out[t].pad[1] = 0;
+}
+
 // Basepoint comb for the throughput committee kernel: comb16[w * E + j] = j * 2^(BITS w) * B,
 // w < WINDOWS, j = 0..2^(BITS-1) (E entries per window; radix 2^22: 12 x 2,097,153 entries =
 // 3.2 GB of the 288 GB HBM): s*B is 12 additions instead of 16 at radix 2^16 (67 MB; 541 -> 590 M

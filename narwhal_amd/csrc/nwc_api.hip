@@ -115,6 +115,8 @@ struct DevCtx {
   nwc::ge_niels_pad* comb_base = nullptr;   // radix-256 basepoint comb (528 KB): latency kernel
   nwc::ge_niels_pad* comb16 = nullptr;      // basepoint comb (radix 2^NWC_BCOMB_BITS, 67 MB at 2^16): k_verify_comb
   nwc::ge_p3* comb16_bases = nullptr;       // its window bases 2^(bits w) B (built at init)
+  nwc::ge_p3* kb_bases = nullptr;           // key comb window bases (scratch of build_key_combs)
+  size_t kb_cap = 0;
   int comb_blocks_per_cu = 1;
   uint32_t* uc_list = nullptr;     // k_verify_comb: equations whose key is not cached
   uint32_t* uc_count = nullptr;
@@ -296,6 +298,27 @@ int require_init() {
   return 0;
 }
 
+// Per-key combs of m keys (KeyComb) into out: window bases first, then one lane per entry.  The
+// caller synchronizes the stream before kb_bases is reused.
+int build_key_combs(DevCtx& d, const nwc::u32* keys, uint32_t m, nwc::ge_niels_pad* out) {
+  if (m == 0) return 0;
+  const size_t need = (size_t)m * nwc::KeyComb::windows;
+  if (need > d.kb_cap) {
+    if (d.kb_bases) HIP_TRY(hipFree(d.kb_bases));
+    d.kb_bases = nullptr;
+    d.kb_cap = 0;
+    HIP_TRY(hipMalloc(&d.kb_bases, need * sizeof(nwc::ge_p3)));
+    d.kb_cap = need;
+  }
+  hipLaunchKernelGGL(nwc::k_comb_key_bases<nwc::KeyComb>, dim3((m + 63) / 64), dim3(64), 0, d.stream, keys, m, d.kb_bases);
+  HIP_TRY(hipGetLastError());
+  const size_t entries = (size_t)m * nwc::COMB_PER_KEY;
+  hipLaunchKernelGGL(nwc::k_build_comb_from_bases<nwc::KeyComb>, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0,
+                     d.stream, (const nwc::ge_p3*)d.kb_bases, m, out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 // NWC_AUTO_KEYS: capacity of the per-device auto key cache (default 256 keys, 20 MB of combs
 // each, allocated on first use; 0 disables it).
 uint32_t auto_keys_cap() {
@@ -374,10 +397,7 @@ int auto_insert(DevCtx& d, const uint8_t* pks, uint64_t n) {
   hipLaunchKernelGGL(nwc::k_build_key_tables, dim3((unsigned)((m * 129 + 255) / 256)), dim3(256), 0, d.stream,
                      d.ak_keys + 8 * (size_t)n0, m, d.ak_tables + (size_t)n0 * 129, d.ak_flags + n0);
   HIP_TRY(hipGetLastError());
-  const size_t entries = (size_t)m * nwc::COMB_PER_KEY;
-  hipLaunchKernelGGL(nwc::k_build_comb<nwc::KeyComb>, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, d.stream,
-                     d.ak_keys + 8 * (size_t)n0, m, d.ak_comb + (size_t)n0 * nwc::COMB_PER_KEY);
-  HIP_TRY(hipGetLastError());
+  if (int rc = build_key_combs(d, d.ak_keys + 8 * (size_t)n0, m, d.ak_comb + (size_t)n0 * nwc::COMB_PER_KEY)) return rc;
   HIP_TRY(hipMemcpyAsync(d.ak_slots, table.data(), 4 * (size_t)slots, hipMemcpyHostToDevice, d.stream));
   // synchronous: the host vectors above are the copy sources
   HIP_TRY(hipStreamSynchronize(d.stream));
@@ -905,6 +925,7 @@ void nwc_shutdown(void) {
     if (d->comb_base) (void)hipFree(d->comb_base);
     if (d->comb16) (void)hipFree(d->comb16);
     if (d->comb16_bases) (void)hipFree(d->comb16_bases);
+    if (d->kb_bases) (void)hipFree(d->kb_bases);
     if (d->pinned) (void)hipHostFree(d->pinned);
     if (d->cc_stakes) (void)hipFree(d->cc_stakes);
     if (d->cc_worker_off) (void)hipFree(d->cc_worker_off);
@@ -1083,9 +1104,7 @@ static int set_committee_locked(const uint8_t* pks, size_t n) {
       // per-key combs for the doubling-free path (radix 2^14: 20 MB per key)
       const size_t entries = n * nwc::COMB_PER_KEY;
       HIP_TRY(hipMalloc(&d.cm_comb, entries * sizeof(nwc::ge_niels_pad)));
-      hipLaunchKernelGGL(nwc::k_build_comb<nwc::KeyComb>, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, d.stream,
-                         d.cm_keys, (nwc::u32)n, d.cm_comb);
-      HIP_TRY(hipGetLastError());
+      if (int rc = build_key_combs(d, d.cm_keys, (uint32_t)n, d.cm_comb)) return rc;
     }
     HIP_TRY(hipStreamSynchronize(d.stream));
     d.cm_n = (uint32_t)n;
