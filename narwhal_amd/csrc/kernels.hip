@@ -28,6 +28,7 @@
 #include "sha512.h"
 #include "lattice.h"
 #include "fe_sliced.h"
+#include "ge_sliced.h"
 
 // Build switches of the half-size ladder (A/B experiments, profiles/r02/experiments.md):
 //   NWC_BASE_FETCH_EARLY  issue a window's first basepoint DMA before its doublings (1) or after
@@ -1417,6 +1418,27 @@ __device__ __forceinline__ void decompress_sliced(const u32 w[8], fe& X, fe& Y, 
   Y = fe_tighten(yl);
   fe_to_words(yl, ycanon);
   ok = correct || flipped;
+}
+
+// Small launches (the first-sight keys of a certificate): one wave per distinct key, its
+// decompression and l*A both limb-sliced (ge_sliced.h): ~160 us per key instead of ~0.8 ms on one
+// lane (tools/microbench/sliced_points.hip).  Same flags and memo as k_tors_eval.
+__global__ __launch_bounds__(64) void k_tors_eval_sliced(TorsArgs t) {
+  const uint32_t N = *t.nuniq;
+  for (uint32_t j = blockIdx.x; j < N; j += gridDim.x) {   // block-uniform: one key per wave
+    const uint32_t h = t.uniq[j];
+    u32 aw[8];
+    load_words8(t.pks + 32 * (uint64_t)t.slots[h], aw);
+    fe X, Y;
+    u32 yc[8];
+    bool ok;
+    decompress_sliced(aw, X, Y, yc, ok);
+    const bool tor = gs_has_torsion(gs_from_affine(X, Y), SC_L);
+    if (threadIdx.x == 0) {
+      t.tflag[h] = (ok && tor) ? 1u : 0u;
+      if (ok) memo_insert(t.memo, aw, tor ? 1u : 0u);
+    }
+  }
 }
 
 __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs ca) {

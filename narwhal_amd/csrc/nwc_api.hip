@@ -483,7 +483,12 @@ int launch_torsion(DevCtx& d, const uint8_t* pks, uint64_t* out_words, uint64_t 
     HIP_TRY(hipMemsetAsync(d.ts_nuniq, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(nwc::k_tors_mark, dim3(grid), dim3(256), 0, s, t);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(nwc::k_tors_eval, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)d.cus * 2)), dim3(256), 0, s, t);
+    if (n <= NWC_WIDE_MAX) {
+      // a certificate's worth of keys: one limb-sliced wave per distinct key (latency)
+      hipLaunchKernelGGL(nwc::k_tors_eval_sliced, dim3((unsigned)n), dim3(64), 0, s, t);
+    } else {
+      hipLaunchKernelGGL(nwc::k_tors_eval, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, (uint64_t)d.cus * 2)), dim3(256), 0, s, t);
+    }
     HIP_TRY(hipGetLastError());
   }
   if (phase & 2) {
