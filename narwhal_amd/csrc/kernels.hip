@@ -1441,6 +1441,159 @@ __global__ __launch_bounds__(64) void k_tors_eval_sliced(TorsArgs t) {
   }
 }
 
+// ---- first-sight small batches: one equation per block, every point operation limb-sliced ----
+// k_verify_cold decides the same half-size equation as verify_half (lattice.h), for calls whose
+// keys no cache holds (a certificate of first-sight keys): wave 0 runs the serial scalar work (s < l,
+// the challenge, the lattice reduction, the digit strings) redundantly on all its lanes, waves 1
+// and 2 decompress A and R limb-sliced side by side; then wave 1 builds both 9-entry tables and
+// runs the whole ladder with ge_sliced.h's two-layer point operations (~0.16 us per layer
+// instead of a ~1,000-instruction serial step per doubling).  Tables live in LDS as 40 limbs per
+// entry (a row-0 lane k < 10 stores limb k of each coordinate; every lane reads its own limb back).
+struct ColdShared {
+  i32 tab[2][TAB_ENTRIES][40];   // [0] multiples of +-A (sign of c), [1] of -R; (YpX, YmX, Z, T2d)
+  i32 ax[10], ay[10], rx[10], ry[10];
+  Digits16 cd, dd;
+  Digits24 el, eh;
+  int W, c_neg, lat_ok, s_ok, a_ok, r_ok, a_small, r_small;
+};
+__device__ __forceinline__ void cold_store(i32* e, const gs_cached& c) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 10) { e[lane] = c.YpX.v; e[10 + lane] = c.YmX.v; e[20 + lane] = c.Z.v; e[30 + lane] = c.T2d.v; }
+}
+// entry e of a table as a cached point; neg: the entry of the negated point (Y+X <-> Y-X, -2dT)
+__device__ __forceinline__ gs_cached cold_load(const i32* e, bool neg) {
+  const int k = fes_lane();
+  const bool live = k < 10;
+  const int kk = live ? k : 0;
+  gs_cached c;
+  const i32 ypx = e[kk], ymx = e[10 + kk];
+  c.YpX.v = live ? (neg ? ymx : ypx) : 0;
+  c.YmX.v = live ? (neg ? ypx : ymx) : 0;
+  c.Z.v = live ? e[20 + kk] : 0;
+  c.T2d.v = live ? (neg ? -e[30 + kk] : e[30 + kk]) : 0;
+  return c;
+}
+// a radix-2^24 basepoint entry (affine Niels, HBM) as a cached point with Z = 1, each lane its limb
+__device__ __forceinline__ gs_cached cold_base_entry(const ge_niels_pad* T, i32 d) {
+  const i32* e = reinterpret_cast<const i32*>(T + (d < 0 ? -d : d));
+  const int k = fes_lane();
+  const bool live = k < 10, neg = d < 0;
+  const int kk = live ? k : 0;
+  const i32 ypx = e[kk], ymx = e[10 + kk], t = e[20 + kk];
+  gs_cached c;
+  c.YpX.v = live ? (neg ? ymx : ypx) : 0;
+  c.YmX.v = live ? (neg ? ypx : ymx) : 0;
+  c.Z.v = k == 0 ? 1 : 0;
+  c.T2d.v = live ? (neg ? -t : t) : 0;
+  return c;
+}
+__device__ __forceinline__ gs_p1p1 gs_cached_to_p1p1(const gs_cached& c) {
+  gs_p1p1 r;
+  r.X = fes_sub(c.YpX, c.YmX);
+  r.Y = fes_add(c.YpX, c.YmX);
+  r.Z = fes_add(c.Z, c.Z);
+  r.T = r.Z;
+  return r;
+}
+// digit of window w (<= W - 2) of a Digits16 string (recode16's layout: nibble w + 41 - W)
+__device__ __forceinline__ i32 digit16_of(const Digits16& x, int w, int W) {
+  const int pos = w + 41 - W;
+  u32 word = x.w[0];
+  _Pragma("unroll") for (int i = 1; i < 5; ++i) word = (pos >> 3) == i ? x.w[i] : word;
+  return (i32)((word >> (4 * (pos & 7))) & 15u) - 8;
+}
+__device__ void cold_table(i32 (*tab)[40], const gs_p3& P) {
+  gs_cached id;
+  id.YpX = fes_from_fe(fe_one()); id.YmX = id.YpX; id.Z = id.YpX; id.T2d.v = 0;
+  cold_store(tab[0], id);
+  const gs_cached p1 = gs_to_cached(P);
+  cold_store(tab[1], p1);
+  gs_p3 pj = gs_to_p3(gs_dbl(gs_p3_to_p2(P)));
+  cold_store(tab[2], gs_to_cached(pj));
+#pragma unroll 1
+  for (int j = 3; j < TAB_ENTRIES; ++j) {
+    pj = gs_to_p3(gs_add_cached(pj, p1));
+    cold_store(tab[j], gs_to_cached(pj));
+  }
+}
+__global__ __launch_bounds__(192) void k_verify_cold(VerifyArgs a) {
+  __shared__ ColdShared sh;
+  const uint64_t i = blockIdx.x;
+  if (i >= a.n) return;   // block-uniform
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  u32 mw[8], aw[8], sgw[16];
+  load_inputs(a, i, mw, aw, sgw);
+  u32 rw[8], sw[8];
+  _Pragma("unroll") for (int q = 0; q < 8; ++q) { rw[q] = sgw[q]; sw[q] = sgw[8 + q]; }
+  if (wave == 0) {
+    u32 kw[8];
+    challenge(rw, aw, mw, kw);
+    const lat::HalfScalars h = lat::reduce(kw);
+    const int W = wave_windows(h.ok ? h.bits : 0);
+    Digits24 el, eh;
+    base_digits(h.d, sw, el, eh);
+    const Digits16 cd = recode16(h.c, W), dd = recode16(h.d, W);
+    if (lane == 0) {
+      sh.W = W; sh.c_neg = h.c_neg; sh.lat_ok = h.ok && W <= HALF_WINDOWS_MAX; sh.s_ok = sc_lt_l(sw);
+      sh.cd = cd; sh.dd = dd; sh.el = el; sh.eh = eh;
+    }
+  } else {
+    fe X, Y;
+    u32 yc[8];
+    bool ok;
+    decompress_sliced(wave == 1 ? aw : rw, X, Y, yc, ok);
+    if (lane == 0) {
+      const bool so = ycanon_is_small_order(yc);
+      _Pragma("unroll") for (int q = 0; q < 10; ++q) {
+        if (wave == 1) { sh.ax[q] = X.v[q]; sh.ay[q] = Y.v[q]; } else { sh.rx[q] = X.v[q]; sh.ry[q] = Y.v[q]; }
+      }
+      if (wave == 1) { sh.a_ok = ok; sh.a_small = so; } else { sh.r_ok = ok; sh.r_small = so; }
+    }
+  }
+  __syncthreads();
+  if (wave != 1) return;
+  fe ax, ay, rx, ry;
+  _Pragma("unroll") for (int q = 0; q < 10; ++q) { ax.v[q] = sh.ax[q]; ay.v[q] = sh.ay[q]; rx.v[q] = sh.rx[q]; ry.v[q] = sh.ry[q]; }
+  // -c A = |c| (c < 0 ? A : -A);  -d R = d (-R)
+  cold_table(sh.tab[0], gs_from_affine(sh.c_neg ? ax : fe_neg(ax), ay));
+  cold_table(sh.tab[1], gs_from_affine(fe_neg(rx), ry));
+  const int W = sh.W;
+  const Digits16 cd = sh.cd, dd = sh.dd;
+  const Digits24 el = sh.el, eh = sh.eh;
+  i32 da = cd.top, dr = dd.top;
+  gs_p1p1 t = gs_cached_to_p1p1(cold_load(sh.tab[0][da], false));
+#pragma unroll 1
+  for (int w = W - 1; w >= 0; --w) {
+    if (w != W - 1) {
+      gs_p2 p2 = gs_to_p2(t);
+#pragma unroll 1
+      for (int j = 0; j < 3; ++j) { t = gs_dbl(p2); p2 = gs_to_p2(t); }
+      t = gs_dbl(p2);
+      da = digit16_of(cd, w, W);
+      t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[0][da < 0 ? -da : da], da < 0));
+      dr = digit16_of(dd, w, W);
+    }
+    t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[1][dr < 0 ? -dr : dr], dr < 0));
+    const int nb = base_window_digits(w);
+#pragma unroll 1
+    for (int side = 0; side < nb; ++side) {
+      const int q = w / 6;
+      const i32 db = side ? eh.d[q + B24_LO_DIGITS - B24_HI_DIGITS] : el.d[q];
+      t = gs_add_cached(gs_to_p3(t), cold_base_entry(a.base24 + (side ? B24_ENTRIES : 0), db));
+    }
+  }
+  const bool ident = gs_is_identity(gs_to_p2(t));
+  if (lane == 0) {
+    const bool strict = a.strict != 0;
+    const bool ok = sh.s_ok && sh.a_ok && sh.r_ok && !(strict && (sh.a_small || sh.r_small));
+    if (!sh.lat_ok || (a.force_fb_every && (i % a.force_fb_every) == 0)) {
+      a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)i;   // decided by k_verify_fallback
+    } else if (ok && ident) {
+      atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));
+    }
+  }
+}
+
 __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs ca) {
   __shared__ fe sh_rx, sh_ry;
   __shared__ int sh_rok;

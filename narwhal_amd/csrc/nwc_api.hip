@@ -498,6 +498,16 @@ int launch_torsion(DevCtx& d, const uint8_t* pks, uint64_t* out_words, uint64_t 
   return 0;
 }
 
+// NWC_COLD=0: small uncached calls take k_verify (one lane per equation) instead of the
+// limb-sliced k_verify_cold (A/B and tests)
+bool cold_path() {
+  static const bool on = [] {
+    const char* e = std::getenv("NWC_COLD");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 // launch_verify flags: the caller checked on the host that every key is in the committee cache,
 // and/or out_words is already zero (both let the latency path run as a single kernel)
 constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4;   // LV_AUTO: the keys are in the auto cache
@@ -588,6 +598,10 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3(lgrid), dim3(256), 0, s, l, ca);
   } else if (half && cm.n) {
     hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a, ca);
+  } else if (half && n <= NWC_WIDE_MAX && cold_path()) {
+    // a small batch no cache covers (first-sight keys): one limb-sliced block per equation
+    if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
+    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(192), 0, s, a);
   } else if (half) {
     hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a, ca);
   } else {
