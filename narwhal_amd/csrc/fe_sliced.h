@@ -93,6 +93,19 @@ FES_DEV fes fes_mul(fes f, fes g) {
   return {live ? out : 0};
 }
 FES_DEV fes fes_sq(fes f) { return fes_mul(f, f); }
+// f * c for a small constant (|c| < 2^17) and a loose f: one carry round, limbs centred like
+// fes_mul's outputs (carries up to 2^18, x 19 into limb 0)
+FES_DEV fes fes_mul_small(fes f, i32 c) {
+  const int k = fes_lane();
+  const bool odd = (k & 1) != 0, live = k < 10;
+  const int w = odd ? 25 : 26;
+  const i64 h = (i64)(live ? f.v : 0) * (i64)c + ((i64)1 << (w - 1));
+  const i32 cy = (i32)(h >> w);
+  const i32 r = (i32)((u32)h & ((1u << w) - 1u)) - (1 << (w - 1));
+  const i32 cy19 = k == 9 ? cy * 19 : 0;
+  const i32 cin = row_shr<1>(cy) | row_shl<9>(cy19);
+  return {live ? r + cin : 0};
+}
 FES_DEV fes fes_add(fes a, fes b) { return {a.v + b.v}; }
 FES_DEV fes fes_sub(fes a, fes b) { return {a.v - b.v}; }
 FES_DEV fes fes_add_small(fes a, i32 c) { return {fes_lane() == 0 ? a.v + c : a.v}; }   // + c (|c| small)

@@ -103,6 +103,27 @@ FES_DEV bool gs_is_identity(const gs_p2& p) {
   return fe_is_zero(fe_from_fes(p.X)) && fe_is_zero(fe_from_fes(fes_sub(p.Y, p.Z)));
 }
 
+// [2^n] P from P's Edwards y alone: Montgomery u = (1 + y) / (1 - y) (Curve25519's birational
+// map; the sign of x drops out), RFC 7748's x-only doubling (t1 = (U + W)^2, t2 = (U - W)^2,
+// U' = t1 t2, W' = (t1 - t2)(t2 + 121666 (t1 - t2))), two layers per doubling.  Projective
+// (U : W); the identity is (U : 0).  No square root: it can start before P is decompressed.
+FES_DEV void gs_xonly_dbl_n(fes y, int n, fes& U, fes& W) {
+  U = fes_add_small(y, 1);
+  W = fes_add_small(fes_neg(y), 1);
+#pragma unroll 1
+  for (int k = 0; k < n; ++k) {
+    const fes s = fes_add(U, W), d = fes_sub(U, W);
+    fes t[4];
+    fes_mul4(s, d, s, d, s, d, s, d, t);
+    const fes e = fes_sub(t[0], t[1]);
+    const fes g = fes_add(t[1], fes_mul_small(e, 121666));
+    fes o[4];
+    fes_mul4(t[0], e, t[0], e, t[1], g, t[1], g, o);
+    U = o[0];
+    W = o[1];
+  }
+}
+
 // l * P != O (ge_has_torsion's double-and-add over l = 2^252 + c0, 252 doublings and 61 cached
 // additions, every step limb-sliced)
 FES_DEV bool gs_has_torsion(const gs_p3& P, const u32 l_words[8]) {

@@ -1455,6 +1455,10 @@ struct ColdShared {
   Digits16 cd, dd;
   Digits24 el, eh;
   int W, c_neg, lat_ok, s_ok, a_ok, r_ok, a_small, r_small;
+  i32 rsum[40];       // wave 0's share of the ladder (the -d R terms), cached
+  i32 dq[3][10];      // batch leaf: [l - 2^252] A (wave 2), projective Edwards
+  i32 tu[2][10];      // batch leaf: u([2^252] A) (wave 3), projective Montgomery (U : W)
+  int ready;          // waves 0-2 done with the scalars and the decompressions
 };
 __device__ __forceinline__ void cold_store(i32* e, const gs_cached& c) {
   const int lane = threadIdx.x & 63;
@@ -1516,15 +1520,47 @@ __device__ void cold_table(i32 (*tab)[40], const gs_p3& P) {
     cold_store(tab[j], gs_to_cached(pj));
   }
 }
-__global__ __launch_bounds__(192) void k_verify_cold(VerifyArgs a) {
+// [m] P for the bits [lo, hi] of the 8-word constant m (left to right; bit hi must be set)
+__device__ gs_p2 gs_mul_bits(const gs_p3& P, const u32 m[8], int hi, int lo) {
+  const gs_cached pc = gs_to_cached(P);
+  gs_p2 acc = gs_p3_to_p2(P);
+#pragma unroll 1
+  for (int bit = hi - 1; bit >= lo; --bit) {
+    gs_p1p1 t = gs_dbl(acc);
+    if ((m[bit >> 5] >> (bit & 31)) & 1u) t = gs_add_cached(gs_to_p3(t), pc);
+    acc = gs_to_p2(t);
+  }
+  return acc;
+}
+__device__ __forceinline__ void cold_store_p2(i32 (*q)[10], const gs_p2& p) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 10) { q[0][lane] = p.X.v; q[1][lane] = p.Y.v; q[2][lane] = p.Z.v; }
+}
+__global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a) {
   __shared__ ColdShared sh;
   const uint64_t i = blockIdx.x;
   if (i >= a.n) return;   // block-uniform
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool leaf = a.strict == 0;
+  if (threadIdx.x == 0) sh.ready = 0;
+  __syncthreads();
   u32 mw[8], aw[8], sgw[16];
   load_inputs(a, i, mw, aw, sgw);
   u32 rw[8], sw[8];
   _Pragma("unroll") for (int q = 0; q < 8; ++q) { rw[q] = sgw[q]; sw[q] = sgw[8 + q]; }
+  if (wave == 3) {
+    // batch leaf: the key's torsion test l A = O  <=>  u([2^252] A) = u([l - 2^252] A) (x-only, so
+    // also (2^252 + l - 2^252) A = O's sign twin, which only a point of small order can meet: then
+    // 2^252 A = O and the twin needs [l - 2^252] A = O, i.e. A = O -- no torsion either way).  The
+    // 252 doublings start from A's y at once, beside everything else.
+    if (leaf) {
+      fes U, W;
+      gs_xonly_dbl_n(fes_from_fe(fe_tighten(fe_from_words(aw))), 252, U, W);
+      if (lane < 10) { sh.tu[0][lane] = U.v; sh.tu[1][lane] = W.v; }
+    }
+    __syncthreads();
+    return;
+  }
   if (wave == 0) {
     u32 kw[8];
     challenge(rw, aw, mw, kw);
@@ -1550,18 +1586,50 @@ __global__ __launch_bounds__(192) void k_verify_cold(VerifyArgs a) {
       if (wave == 1) { sh.a_ok = ok; sh.a_small = so; } else { sh.r_ok = ok; sh.r_small = so; }
     }
   }
-  __syncthreads();
-  if (wave != 1) return;
-  fe ax, ay, rx, ry;
-  _Pragma("unroll") for (int q = 0; q < 10; ++q) { ax.v[q] = sh.ax[q]; ay.v[q] = sh.ay[q]; rx.v[q] = sh.rx[q]; ry.v[q] = sh.ry[q]; }
-  // -c A = |c| (c < 0 ? A : -A);  -d R = d (-R)
-  cold_table(sh.tab[0], gs_from_affine(sh.c_neg ? ax : fe_neg(ax), ay));
-  cold_table(sh.tab[1], gs_from_affine(fe_neg(rx), ry));
+  // waves 0-2 meet without wave 3 (still doubling): an LDS counter, release / acquire
+  if (lane == 0) __hip_atomic_fetch_add(&sh.ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(&sh.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 3) __builtin_amdgcn_s_sleep(1);
   const int W = sh.W;
-  const Digits16 cd = sh.cd, dd = sh.dd;
+  if (wave == 2) {
+    if (leaf) {
+      fe ax, ay;
+      _Pragma("unroll") for (int q = 0; q < 10; ++q) { ax.v[q] = sh.ax[q]; ay.v[q] = sh.ay[q]; }
+      const gs_p2 r = gs_mul_bits(gs_from_affine(ax, ay), SC_L, 124, 0);   // l - 2^252 < 2^125
+      cold_store_p2(sh.dq, r);
+    }
+    __syncthreads();
+    return;
+  }
+  if (wave == 0) {
+    // the -d R terms: their own table and ladder (same windows and doublings as wave 1's)
+    fe rx, ry;
+    _Pragma("unroll") for (int q = 0; q < 10; ++q) { rx.v[q] = sh.rx[q]; ry.v[q] = sh.ry[q]; }
+    cold_table(sh.tab[1], gs_from_affine(fe_neg(rx), ry));
+    const Digits16 dd = sh.dd;
+    i32 dr = dd.top;
+    gs_p1p1 t = gs_cached_to_p1p1(cold_load(sh.tab[1][dr < 0 ? -dr : dr], dr < 0));
+#pragma unroll 1
+    for (int w = W - 2; w >= 0; --w) {
+      gs_p2 p2 = gs_to_p2(t);
+#pragma unroll 1
+      for (int j = 0; j < 3; ++j) { t = gs_dbl(p2); p2 = gs_to_p2(t); }
+      t = gs_dbl(p2);
+      dr = digit16_of(dd, w, W);
+      t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[1][dr < 0 ? -dr : dr], dr < 0));
+    }
+    cold_store(sh.rsum, gs_to_cached(gs_to_p3(t)));
+    __syncthreads();
+    return;
+  }
+  // wave 1: the -c A and s B terms
+  fe ax, ay;
+  _Pragma("unroll") for (int q = 0; q < 10; ++q) { ax.v[q] = sh.ax[q]; ay.v[q] = sh.ay[q]; }
+  // -c A = |c| (c < 0 ? A : -A)
+  cold_table(sh.tab[0], gs_from_affine(sh.c_neg ? ax : fe_neg(ax), ay));
+  const Digits16 cd = sh.cd;
   const Digits24 el = sh.el, eh = sh.eh;
-  i32 da = cd.top, dr = dd.top;
-  gs_p1p1 t = gs_cached_to_p1p1(cold_load(sh.tab[0][da], false));
+  i32 da = cd.top;
+  gs_p1p1 t = gs_cached_to_p1p1(cold_load(sh.tab[0][da < 0 ? -da : da], da < 0));
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     if (w != W - 1) {
@@ -1571,9 +1639,7 @@ __global__ __launch_bounds__(192) void k_verify_cold(VerifyArgs a) {
       t = gs_dbl(p2);
       da = digit16_of(cd, w, W);
       t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[0][da < 0 ? -da : da], da < 0));
-      dr = digit16_of(dd, w, W);
     }
-    t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[1][dr < 0 ? -dr : dr], dr < 0));
     const int nb = base_window_digits(w);
 #pragma unroll 1
     for (int side = 0; side < nb; ++side) {
@@ -1582,11 +1648,25 @@ __global__ __launch_bounds__(192) void k_verify_cold(VerifyArgs a) {
       t = gs_add_cached(gs_to_p3(t), cold_base_entry(a.base24 + (side ? B24_ENTRIES : 0), db));
     }
   }
+  __syncthreads();   // wave 0's -d R share, waves 2 and 3's halves of the torsion test
+  t = gs_add_cached(gs_to_p3(t), cold_load(sh.rsum, false));
   const bool ident = gs_is_identity(gs_to_p2(t));
+  bool torsion = false;
+  if (leaf) {
+    // u([l - 2^252] A) = (Z + Y : Z - Y);  same u  <=>  U (Z - Y) = W (Z + Y)
+    fe U, Wm, Y, Z;
+    _Pragma("unroll") for (int q = 0; q < 10; ++q) {
+      U.v[q] = sh.tu[0][q]; Wm.v[q] = sh.tu[1][q]; Y.v[q] = sh.dq[1][q]; Z.v[q] = sh.dq[2][q];
+    }
+    const bool same = fe_is_zero(fe_sub(fe_mul(U, fe_sub(Z, Y)), fe_mul(Wm, fe_add(Z, Y))));
+    torsion = sh.a_ok && !same;
+  }
   if (lane == 0) {
     const bool strict = a.strict != 0;
     const bool ok = sh.s_ok && sh.a_ok && sh.r_ok && !(strict && (sh.a_small || sh.r_small));
-    if (!sh.lat_ok || (a.force_fb_every && (i % a.force_fb_every) == 0)) {
+    if (torsion) {
+      // randomized domain (a key with torsion): Err, whatever the equation says
+    } else if (!sh.lat_ok || (a.force_fb_every && (i % a.force_fb_every) == 0)) {
       a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)i;   // decided by k_verify_fallback
     } else if (ok && ident) {
       atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));

@@ -573,7 +573,10 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const bool half = path != VPath::Full;
   // small batch-leaf launches outside the comb path: the keys' torsion test (one long serial
   // lane per new key) runs on the side stream beside the verification instead of after it
-  const bool tors_beside = !strict && !comb && n <= NWC_WIDE_MAX;
+  // a small batch no cache covers (first-sight keys): one limb-sliced block per equation, the
+  // batch leaf's torsion test inside it
+  const bool cold = half && !comb && !cm.n && n <= NWC_WIDE_MAX && cold_path();
+  const bool tors_beside = !strict && !comb && n <= NWC_WIDE_MAX && !cold;
   if (tors_beside) {
     HIP_TRY(hipEventRecord(d.ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(d.side, d.ev_fork, 0));
@@ -598,10 +601,9 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3(lgrid), dim3(256), 0, s, l, ca);
   } else if (half && cm.n) {
     hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a, ca);
-  } else if (half && n <= NWC_WIDE_MAX && cold_path()) {
-    // a small batch no cache covers (first-sight keys): one limb-sliced block per equation
+  } else if (cold) {
     if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
-    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(192), 0, s, a);
+    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(256), 0, s, a);
   } else if (half) {
     hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a, ca);
   } else {
@@ -619,7 +621,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   if (tors_beside) {
     HIP_TRY(hipStreamWaitEvent(s, d.ev_join, 0));
     if (int rc = launch_torsion(d, pks, out_words, n, nullptr, nullptr, cm, s, 2, 1)) return rc;
-  } else if (!strict) {
+  } else if (!strict && !cold) {
     if (int rc = launch_torsion(d, pks, out_words, n, comb ? d.uc_list : nullptr, comb ? d.uc_count : nullptr, cm, s))
       return rc;
   }
