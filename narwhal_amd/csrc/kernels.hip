@@ -1536,7 +1536,10 @@ __device__ __forceinline__ void cold_store_p2(i32 (*q)[10], const gs_p2& p) {
   const int lane = threadIdx.x & 63;
   if (lane < 10) { q[0][lane] = p.X.v; q[1][lane] = p.Y.v; q[2][lane] = p.Z.v; }
 }
-__global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a) {
+// vbytes != nullptr: zero-copy launch (inputs in pinned host memory), one verdict byte per
+// equation stored straight to the host like k_verify_comb_wide's (bit 7 written, bit 0 valid, bit
+// 1 = the reduction failed: the host re-runs the staged path, whose fallback kernel decides it)
+__global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, uint8_t* vbytes) {
   __shared__ ColdShared sh;
   const uint64_t i = blockIdx.x;
   if (i >= a.n) return;   // block-uniform
@@ -1664,9 +1667,13 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a) {
   if (lane == 0) {
     const bool strict = a.strict != 0;
     const bool ok = sh.s_ok && sh.a_ok && sh.r_ok && !(strict && (sh.a_small || sh.r_small));
-    if (torsion) {
+    const bool fb = !torsion && (!sh.lat_ok || (a.force_fb_every && (i % a.force_fb_every) == 0));
+    if (vbytes) {
+      __hip_atomic_store(vbytes + i, (uint8_t)(0x80u | (!torsion && !fb && ok && ident ? 1u : 0u) | (fb ? 2u : 0u)),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (torsion) {
       // randomized domain (a key with torsion): Err, whatever the equation says
-    } else if (!sh.lat_ok || (a.force_fb_every && (i % a.force_fb_every) == 0)) {
+    } else if (fb) {
       a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)i;   // decided by k_verify_fallback
     } else if (ok && ident) {
       atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));

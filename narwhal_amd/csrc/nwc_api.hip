@@ -529,6 +529,19 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     HIP_TRY(hipGetLastError());
     return 0;
   }
+  static const uint32_t force_every = [] {
+    const char* e = std::getenv("NWC_FORCE_FALLBACK_EVERY");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+  }();
+  if (vbytes && !(flags & LV_ALL_CACHED)) {
+    // zero-copy cold launch (the caller checked: no committee cache, n <= NWC_WIDE_MAX, default
+    // path, cold kernel on): no scratch, no fallback launch, verdict bytes straight to the host
+    const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24,
+                            d.scratch, d.fb_list, d.fb_count, force_every, nwc::Committee{}};
+    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(256), 0, s, a, vbytes);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   const bool comb = path == VPath::Default && d.cm_n && d.cm_comb;
   if (comb && n <= NWC_WIDE_MAX && (flags & LV_ALL_CACHED)) {
     // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none).
@@ -561,10 +574,6 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   }
   if (int rc = ensure_scratch(d, need, n)) return rc;
   HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
-  static const uint32_t force_every = [] {
-    const char* e = std::getenv("NWC_FORCE_FALLBACK_EVERY");
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
-  }();
   const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
   nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
@@ -603,7 +612,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a, ca);
   } else if (cold) {
     if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
-    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(256), 0, s, a, (uint8_t*)nullptr);
   } else if (half) {
     hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a, ca);
   } else {
@@ -749,10 +758,14 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
       const char* e = std::getenv("NWC_ZERO_COPY");
       return !(e && std::strcmp(e, "0") == 0);
     }();
-    if (zero_copy && (fl & LV_ALL_CACHED) && n <= NWC_WIDE_MAX && vb_off + n <= NWC_PINNED_STAGE_MAX &&
-        verify_path() == VPath::Default && (fl & LV_AUTO ? d.ak_comb != nullptr : d.cm_comb != nullptr)) {
+    const bool zc_ok = zero_copy && n <= NWC_WIDE_MAX && vb_off + n <= NWC_PINNED_STAGE_MAX &&
+                       verify_path() == VPath::Default;
+    const bool zc_cached = zc_ok && (fl & LV_ALL_CACHED) && (fl & LV_AUTO ? d.ak_comb != nullptr : d.cm_comb != nullptr);
+    const bool zc_cold = zc_ok && !(fl & LV_ALL_CACHED) && !d.cm_n && cold_path();
+    if (zc_cached || zc_cold) {
       // every key cached: the latency kernel reads the staged inputs in place from pinned host
-      // memory and stores one verdict byte per equation there -- no DMA copy either way
+      // memory and stores one verdict byte per equation there -- no DMA copy either way; no key
+      // cached (first sight): the cold kernel, the same way
       uint8_t* hb = h + vb_off;
       std::memset(hb, 0, n);
       auto dev = [&](const void* p) { return p ? d.pinned_dev + ((const uint8_t*)p - d.arena) : nullptr; };
@@ -789,8 +802,9 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
         if (hb[i] & 1) out_words[i >> 6] |= 1ull << (i & 63);
         missing = missing || (hb[i] & 2);
       }
-      if (!missing) return 0;
-      // a key was missing on the device after all: stage the inputs and run the general path
+      if (!missing) return zc_cold ? auto_insert(d, pks + 32 * lo, n) : 0;
+      // a key was missing on the device after all (cold: a reduction failed): stage the inputs
+      // and run the general path
       std::fill(out_words.begin(), out_words.end(), 0);
       fl &= ~(LV_ALL_CACHED | LV_AUTO);
       HIP_TRY(hipMemcpyAsync(d.arena, h, (size_t)((uint8_t*)dout - d.arena) + 8 * (words + 1), hipMemcpyHostToDevice,

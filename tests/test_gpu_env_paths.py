@@ -1,7 +1,10 @@
 """Small-call paths selected by process-wide switches, each in its own process (libnwc reads them
 once): NWC_ZERO_COPY=0 (staged H2D/D2H copies instead of the zero-copy latency launch),
-NWC_SPIN_WAIT=0 (the zero-copy launch waited on its stream instead of polled) and NWC_AUTO_KEYS=2
-(an auto key cache that fills up after two keys).  Verdicts and bad-vote sets
+NWC_SPIN_WAIT=0 (the zero-copy launch waited on its stream instead of polled), NWC_AUTO_KEYS=2
+(an auto key cache that fills up after two keys), NWC_COLD=0 (first-sight calls on the one-lane
+ladder with the torsion test beside it instead of k_verify_cold) and NWC_FORCE_FALLBACK_EVERY=2
+(every other equation treated as a failed reduction: the zero-copy cold launch hands the call back
+to the staged path, whose fallback kernel decides those equations).  Verdicts and bad-vote sets
 must equal the golden fixtures on every path, with and without the committee cache."""
 import json
 import os
@@ -16,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("env", [{"NWC_ZERO_COPY": "0"}, {"NWC_SPIN_WAIT": "0"}, {"NWC_AUTO_KEYS": "2"},
-                                 {"NWC_AUTO_KEYS": "0"}])
+                                 {"NWC_AUTO_KEYS": "0"}, {"NWC_COLD": "0"}, {"NWC_FORCE_FALLBACK_EVERY": "2"}])
 def test_small_call_paths_match_fixtures(env, golden_verify, golden_batch, tmp_path):
     out = tmp_path / "out.json"
     subprocess.run([sys.executable, os.path.join(ROOT, "tests", "env_paths_helper.py"), str(out), ROOT],
