@@ -887,7 +887,8 @@ __device__ bool verify_full(const u32 mw[8], const u32 aw[8], const u32 sigw[16]
 }
 
 // e_B = d * s mod l, split at 2^141 into radix-2^24 digit queues (el, eh)
-__device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digits24& el, Digits24& eh) {
+// eb = d s mod l (d < 2^160)
+__device__ __forceinline__ void ds_mod_l(const u32 d[5], const u32 s[8], u32 eb[8]) {
   u32 prod[16];
   _Pragma("unroll") for (int i = 0; i < 16; ++i) prod[i] = 0;
   _Pragma("unroll") for (int x = 0; x < 5; ++x) {
@@ -899,8 +900,11 @@ __device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digi
     }
     prod[x + 8] = (u32)carry;
   }
-  u32 eb[8];
   sc_reduce512(prod, eb);
+}
+__device__ __forceinline__ void base_digits(const u32 d[5], const u32 s[8], Digits24& el, Digits24& eh) {
+  u32 eb[8];
+  ds_mod_l(d, s, eb);
   constexpr int SH = B24_SPLIT_BITS - 128;
   u32 lo[5], hi[5];
   _Pragma("unroll") for (int i = 0; i < 4; ++i) lo[i] = eb[i];
@@ -1443,19 +1447,23 @@ __global__ __launch_bounds__(64) void k_tors_eval_sliced(TorsArgs t) {
 
 // ---- first-sight small batches: one equation per block, every point operation limb-sliced ----
 // k_verify_cold decides the same half-size equation as verify_half (lattice.h), for calls whose
-// keys no cache holds (a certificate of first-sight keys): wave 0 runs the serial scalar work (s < l,
-// the challenge, the lattice reduction, the digit strings) redundantly on all its lanes, waves 1
-// and 2 decompress A and R limb-sliced side by side; then wave 1 builds both 9-entry tables and
-// runs the whole ladder with ge_sliced.h's two-layer point operations (~0.16 us per layer
-// instead of a ~1,000-instruction serial step per doubling).  Tables live in LDS as 40 limbs per
-// entry (a row-0 lane k < 10 stores limb k of each coordinate; every lane reads its own limb back).
+// keys no cache holds (a certificate of first-sight keys), one 4-wave block per equation with
+// every point operation limb-sliced (ge_sliced.h: two layers of ~0.19 us per doubling or addition
+// instead of a ~1,000-instruction serial step).  Phase 1: wave 0 runs the scalar work (s < l, the
+// challenge, the lattice reduction, d s mod l, the digit strings) on all its lanes, waves 1 and 2
+// decompress A and R; wave 3 (batch leaf) starts u([2^252] A) from A's y at once.  Phase 2: wave 0
+// the -d R share of the ladder, wave 1 the -c A share, wave 2 (batch leaf) [l - 2^252] A, wave 3
+// [d s mod l] B from the basepoint comb; wave 1 adds the shares and decides.  Tables live in LDS
+// as 40 limbs per entry (a row-0 lane k < 10 stores limb k of each coordinate; every lane reads
+// its own limb back).
 struct ColdShared {
-  i32 tab[2][TAB_ENTRIES][40];   // [0] multiples of +-A (sign of c), [1] of -R; (YpX, YmX, Z, T2d)
+  i32 tab[3][TAB_ENTRIES][40];   // [0] multiples of +-A (sign of c), [1] of -R, [2] of A; (YpX, YmX, Z, T2d)
   i32 ax[10], ay[10], rx[10], ry[10];
   Digits16 cd, dd;
-  Digits24 el, eh;
+  u32 bs[8];          // d s mod l: the basepoint's scalar
   int W, c_neg, lat_ok, s_ok, a_ok, r_ok, a_small, r_small;
   i32 rsum[40];       // wave 0's share of the ladder (the -d R terms), cached
+  i32 bsum[40];       // wave 3's [d s mod l] B (basepoint comb, no doublings), cached
   i32 dq[3][10];      // batch leaf: [l - 2^252] A (wave 2), projective Edwards
   i32 tu[2][10];      // batch leaf: u([2^252] A) (wave 3), projective Montgomery (U : W)
   int ready;          // waves 0-2 done with the scalars and the decompressions
@@ -1539,7 +1547,8 @@ __device__ __forceinline__ void cold_store_p2(i32 (*q)[10], const gs_p2& p) {
 // vbytes != nullptr: zero-copy launch (inputs in pinned host memory), one verdict byte per
 // equation stored straight to the host like k_verify_comb_wide's (bit 7 written, bit 0 valid, bit
 // 1 = the reduction failed: the host re-runs the staged path, whose fallback kernel decides it)
-__global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, uint8_t* vbytes) {
+__global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niels_pad* __restrict__ comb16,
+                                                    uint8_t* vbytes) {
   __shared__ ColdShared sh;
   const uint64_t i = blockIdx.x;
   if (i >= a.n) return;   // block-uniform
@@ -1561,6 +1570,20 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, uint8_t* vbyt
       gs_xonly_dbl_n(fes_from_fe(fe_tighten(fe_from_words(aw))), 252, U, W);
       if (lane < 10) { sh.tu[0][lane] = U.v; sh.tu[1][lane] = W.v; }
     }
+    // then [d s mod l] B from the radix-2^22 basepoint comb: 12 entries, 11 additions, no
+    // doublings (wave 0 has published the scalar by now in a batch leaf; a strict call waits here)
+    while (__hip_atomic_load(&sh.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 3) __builtin_amdgcn_s_sleep(1);
+    u32 eb[8], sd[9];
+    _Pragma("unroll") for (int q = 0; q < 8; ++q) eb[q] = sh.bs[q];
+    sc_recode_radix<NWC_BCOMB_BITS, COMB16_WINDOWS>(eb, sd);
+    i32 db = digit_at<NWC_BCOMB_BITS>(sd, COMB16_WINDOWS - 1);
+    gs_p1p1 t = gs_cached_to_p1p1(cold_base_entry(comb16 + (size_t)(COMB16_WINDOWS - 1) * COMB16_ENTRIES, db));
+#pragma unroll 1
+    for (int w = COMB16_WINDOWS - 2; w >= 0; --w) {
+      db = digit_at<NWC_BCOMB_BITS>(sd, w);
+      t = gs_add_cached(gs_to_p3(t), cold_base_entry(comb16 + (size_t)w * COMB16_ENTRIES, db));
+    }
+    cold_store(sh.bsum, gs_to_cached(gs_to_p3(t)));
     __syncthreads();
     return;
   }
@@ -1569,12 +1592,13 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, uint8_t* vbyt
     challenge(rw, aw, mw, kw);
     const lat::HalfScalars h = lat::reduce(kw);
     const int W = wave_windows(h.ok ? h.bits : 0);
-    Digits24 el, eh;
-    base_digits(h.d, sw, el, eh);
+    u32 eb[8];
+    ds_mod_l(h.d, sw, eb);
     const Digits16 cd = recode16(h.c, W), dd = recode16(h.d, W);
     if (lane == 0) {
       sh.W = W; sh.c_neg = h.c_neg; sh.lat_ok = h.ok && W <= HALF_WINDOWS_MAX; sh.s_ok = sc_lt_l(sw);
-      sh.cd = cd; sh.dd = dd; sh.el = el; sh.eh = eh;
+      sh.cd = cd; sh.dd = dd;
+      _Pragma("unroll") for (int q = 0; q < 8; ++q) sh.bs[q] = eb[q];
     }
   } else {
     fe X, Y;
@@ -1597,8 +1621,22 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, uint8_t* vbyt
     if (leaf) {
       fe ax, ay;
       _Pragma("unroll") for (int q = 0; q < 10; ++q) { ax.v[q] = sh.ax[q]; ay.v[q] = sh.ay[q]; }
-      const gs_p2 r = gs_mul_bits(gs_from_affine(ax, ay), SC_L, 124, 0);   // l - 2^252 < 2^125
-      cold_store_p2(sh.dq, r);
+      // [l - 2^252] A, l - 2^252 < 2^125: signed radix-16 digits (32 windows) over A's own table
+      cold_table(sh.tab[2], gs_from_affine(ax, ay));
+      const u32 delta[5] = {SC_L[0], SC_L[1], SC_L[2], SC_L[3], 0u};
+      const Digits16 dg = recode16(delta, 32);
+      i32 dv = dg.top;
+      gs_p1p1 t = gs_cached_to_p1p1(cold_load(sh.tab[2][dv < 0 ? -dv : dv], dv < 0));
+#pragma unroll 1
+      for (int w = 30; w >= 0; --w) {
+        gs_p2 p2 = gs_to_p2(t);
+#pragma unroll 1
+        for (int j = 0; j < 3; ++j) { t = gs_dbl(p2); p2 = gs_to_p2(t); }
+        t = gs_dbl(p2);
+        dv = digit16_of(dg, w, 32);
+        t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[2][dv < 0 ? -dv : dv], dv < 0));
+      }
+      cold_store_p2(sh.dq, gs_to_p2(t));
     }
     __syncthreads();
     return;
@@ -1630,7 +1668,6 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, uint8_t* vbyt
   // -c A = |c| (c < 0 ? A : -A)
   cold_table(sh.tab[0], gs_from_affine(sh.c_neg ? ax : fe_neg(ax), ay));
   const Digits16 cd = sh.cd;
-  const Digits24 el = sh.el, eh = sh.eh;
   i32 da = cd.top;
   gs_p1p1 t = gs_cached_to_p1p1(cold_load(sh.tab[0][da < 0 ? -da : da], da < 0));
 #pragma unroll 1
@@ -1643,16 +1680,10 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, uint8_t* vbyt
       da = digit16_of(cd, w, W);
       t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[0][da < 0 ? -da : da], da < 0));
     }
-    const int nb = base_window_digits(w);
-#pragma unroll 1
-    for (int side = 0; side < nb; ++side) {
-      const int q = w / 6;
-      const i32 db = side ? eh.d[q + B24_LO_DIGITS - B24_HI_DIGITS] : el.d[q];
-      t = gs_add_cached(gs_to_p3(t), cold_base_entry(a.base24 + (side ? B24_ENTRIES : 0), db));
-    }
   }
-  __syncthreads();   // wave 0's -d R share, waves 2 and 3's halves of the torsion test
+  __syncthreads();   // wave 0's -d R share, wave 3's s B, waves 2 and 3's halves of the torsion test
   t = gs_add_cached(gs_to_p3(t), cold_load(sh.rsum, false));
+  t = gs_add_cached(gs_to_p3(t), cold_load(sh.bsum, false));
   const bool ident = gs_is_identity(gs_to_p2(t));
   bool torsion = false;
   if (leaf) {

@@ -538,7 +538,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     // path, cold kernel on): no scratch, no fallback launch, verdict bytes straight to the host
     const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24,
                             d.scratch, d.fb_list, d.fb_count, force_every, nwc::Committee{}};
-    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(256), 0, s, a, vbytes);
+    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(256), 0, s, a, (const nwc::ge_niels_pad*)d.comb16, vbytes);
     HIP_TRY(hipGetLastError());
     return 0;
   }
@@ -612,7 +612,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a, ca);
   } else if (cold) {
     if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
-    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(256), 0, s, a, (uint8_t*)nullptr);
+    hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(256), 0, s, a, (const nwc::ge_niels_pad*)d.comb16,
+                       (uint8_t*)nullptr);
   } else if (half) {
     hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a, ca);
   } else {
