@@ -1540,6 +1540,25 @@ __device__ gs_p2 gs_mul_bits(const gs_p3& P, const u32 m[8], int hi, int lo) {
   }
   return acc;
 }
+#ifndef NWC_COLD_BSUM_WAVE0
+#define NWC_COLD_BSUM_WAVE0 0
+#endif
+#ifndef NWC_COLD_TIMING
+#define NWC_COLD_TIMING 0   // 1: block 0 prints per-wave phase times (A/B builds only)
+#endif
+// [e] B from the radix-2^22 basepoint comb (COMB16_WINDOWS entries, one addition each), cached
+__device__ gs_cached cold_comb_sum(const ge_niels_pad* comb16, const u32 e[8]) {
+  u32 sd[9];
+  sc_recode_radix<NWC_BCOMB_BITS, COMB16_WINDOWS>(e, sd);
+  i32 db = digit_at<NWC_BCOMB_BITS>(sd, COMB16_WINDOWS - 1);
+  gs_p1p1 t = gs_cached_to_p1p1(cold_base_entry(comb16 + (size_t)(COMB16_WINDOWS - 1) * COMB16_ENTRIES, db));
+#pragma unroll 1
+  for (int w = COMB16_WINDOWS - 2; w >= 0; --w) {
+    db = digit_at<NWC_BCOMB_BITS>(sd, w);
+    t = gs_add_cached(gs_to_p3(t), cold_base_entry(comb16 + (size_t)w * COMB16_ENTRIES, db));
+  }
+  return gs_to_cached(gs_to_p3(t));
+}
 __device__ __forceinline__ void cold_store_p2(i32 (*q)[10], const gs_p2& p) {
   const int lane = threadIdx.x & 63;
   if (lane < 10) { q[0][lane] = p.X.v; q[1][lane] = p.Y.v; q[2][lane] = p.Z.v; }
@@ -1556,6 +1575,14 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
   const bool leaf = a.strict == 0;
   if (threadIdx.x == 0) sh.ready = 0;
   __syncthreads();
+#if NWC_COLD_TIMING
+  const uint64_t ct0 = wall_clock64();
+  __shared__ uint32_t ctv[4][4];
+  int ctn = 0;
+#define CT(tag) do { if (lane == 0) ctv[wave][ctn] = (uint32_t)(wall_clock64() - ct0); ++ctn; } while (0)
+#else
+#define CT(tag) do {} while (0)
+#endif
   u32 mw[8], aw[8], sgw[16];
   load_inputs(a, i, mw, aw, sgw);
   u32 rw[8], sw[8];
@@ -1570,20 +1597,16 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
       gs_xonly_dbl_n(fes_from_fe(fe_tighten(fe_from_words(aw))), 252, U, W);
       if (lane < 10) { sh.tu[0][lane] = U.v; sh.tu[1][lane] = W.v; }
     }
+    CT("xonly");
+#if !NWC_COLD_BSUM_WAVE0
     // then [d s mod l] B from the radix-2^22 basepoint comb: 12 entries, 11 additions, no
     // doublings (wave 0 has published the scalar by now in a batch leaf; a strict call waits here)
     while (__hip_atomic_load(&sh.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 3) __builtin_amdgcn_s_sleep(1);
-    u32 eb[8], sd[9];
+    u32 eb[8];
     _Pragma("unroll") for (int q = 0; q < 8; ++q) eb[q] = sh.bs[q];
-    sc_recode_radix<NWC_BCOMB_BITS, COMB16_WINDOWS>(eb, sd);
-    i32 db = digit_at<NWC_BCOMB_BITS>(sd, COMB16_WINDOWS - 1);
-    gs_p1p1 t = gs_cached_to_p1p1(cold_base_entry(comb16 + (size_t)(COMB16_WINDOWS - 1) * COMB16_ENTRIES, db));
-#pragma unroll 1
-    for (int w = COMB16_WINDOWS - 2; w >= 0; --w) {
-      db = digit_at<NWC_BCOMB_BITS>(sd, w);
-      t = gs_add_cached(gs_to_p3(t), cold_base_entry(comb16 + (size_t)w * COMB16_ENTRIES, db));
-    }
-    cold_store(sh.bsum, gs_to_cached(gs_to_p3(t)));
+    cold_store(sh.bsum, cold_comb_sum(comb16, eb));
+#endif
+    CT("bsum");
     __syncthreads();
     return;
   }
@@ -1600,6 +1623,9 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
       sh.cd = cd; sh.dd = dd;
       _Pragma("unroll") for (int q = 0; q < 8; ++q) sh.bs[q] = eb[q];
     }
+#if NWC_COLD_BSUM_WAVE0
+    cold_store(sh.bsum, cold_comb_sum(comb16, eb));   // A/B: the comb sum in wave 0's phase 1
+#endif
   } else {
     fe X, Y;
     u32 yc[8];
@@ -1613,6 +1639,7 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
       if (wave == 1) { sh.a_ok = ok; sh.a_small = so; } else { sh.r_ok = ok; sh.r_small = so; }
     }
   }
+  CT("phase1");
   // waves 0-2 meet without wave 3 (still doubling): an LDS counter, release / acquire
   if (lane == 0) __hip_atomic_fetch_add(&sh.ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   while (__hip_atomic_load(&sh.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 3) __builtin_amdgcn_s_sleep(1);
@@ -1637,6 +1664,7 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
         t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[2][dv < 0 ? -dv : dv], dv < 0));
       }
       cold_store_p2(sh.dq, gs_to_p2(t));
+      CT("deltaA");
     }
     __syncthreads();
     return;
@@ -1659,6 +1687,7 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
       t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[1][dr < 0 ? -dr : dr], dr < 0));
     }
     cold_store(sh.rsum, gs_to_cached(gs_to_p3(t)));
+    CT("Rshare");
     __syncthreads();
     return;
   }
@@ -1681,10 +1710,17 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
       t = gs_add_cached(gs_to_p3(t), cold_load(sh.tab[0][da < 0 ? -da : da], da < 0));
     }
   }
+  CT("Ashare");
   __syncthreads();   // wave 0's -d R share, wave 3's s B, waves 2 and 3's halves of the torsion test
   t = gs_add_cached(gs_to_p3(t), cold_load(sh.rsum, false));
   t = gs_add_cached(gs_to_p3(t), cold_load(sh.bsum, false));
   const bool ident = gs_is_identity(gs_to_p2(t));
+  CT("final");
+#if NWC_COLD_TIMING
+  if (blockIdx.x == 0 && lane == 0)
+    printf("cold ticks w0 %u %u | w1 %u %u %u | w2 %u %u | w3 %u %u\n", ctv[0][0], ctv[0][1], ctv[1][0], ctv[1][1],
+           ctv[1][2], ctv[2][0], ctv[2][1], ctv[3][0], ctv[3][1]);
+#endif
   bool torsion = false;
   if (leaf) {
     // u([l - 2^252] A) = (Z + Y : Z - Y);  same u  <=>  U (Z - Y) = W (Z + Y)
