@@ -4,7 +4,10 @@ has (bit flips in R / s / A / msg, s + l, small-order and non-canonical R and A 
 and A bytes, the golden edge cases tiled in), verified on the GPU in strict and batch-leaf mode
 and compared verdict by verdict with the CPU restatement (oracle/, multithreaded).
 
-    python tests/soak.py [--n 8388608] [--chunk 1048576] [--committee K] [--out gpurun_out/soak.json]
+    python tests/soak.py [--n 8388608] [--chunk 1048576] [--committee K] [--call C] [--out gpurun_out/soak.json]
+
+--call C verifies each chunk in device calls of at most C equations (C <= 1024 without a
+committee: the cold kernel, k_verify_cold, one block per equation).
 
 Test infrastructure (it runs the oracle), kept under tests/ like the oracle helpers; not part of
 the default pytest run (minutes of CPU oracle time).
@@ -76,6 +79,7 @@ def main():
     ap.add_argument("--committee", type=int, default=0,
                     help="K > 0: signers drawn from K keys registered with nwc_set_committee (comb path, "
                          "cached ladder and the uncached list for mutated keys)")
+    ap.add_argument("--call", type=int, default=0, help="C > 0: device calls of at most C equations")
     args = ap.parse_args()
     lib = _lib.load()
     if args.committee:
@@ -107,8 +111,12 @@ def main():
         m, p, s = (t.cpu().numpy().copy() for t in (msgs, pks, sigs))
         kind = mutate(rng, m, p, s, golden)
         tm, tp, ts = (torch.from_numpy(x).cuda() for x in (m, p, s))
-        gs = device.unpack_bits(device.verify(tm, tp, ts, strict=True), n)
-        gl = device.unpack_bits(device.verify(tm, tp, ts, strict=False), n)
+        def run(strict):
+            step = args.call or n
+            return np.concatenate([device.unpack_bits(device.verify(tm[a:a + step], tp[a:a + step], ts[a:a + step],
+                                                                    strict=strict), min(step, n - a))
+                                   for a in range(0, n, step)])
+        gs, gl = run(True), run(False)
         os_ = orc.strict_many(m, p, s, threads=threads)
         ol = orc.leaf_many(m, p, s, threads=threads)
         for j in np.nonzero((gs != os_) | (gl != ol))[0][:20]:
@@ -126,7 +134,7 @@ def main():
         done += n
         print("soak %d / %d  %.0f s" % (done, args.n, time.time() - t0), file=sys.stderr, flush=True)
     total = {k: sum(v[k] for v in stats.values()) for k in ("n", "strict_mismatch", "leaf_mismatch")}
-    out = {"triples": args.n, "committee": args.committee, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
+    out = {"triples": args.n, "committee": args.committee, "call": args.call, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
            "mismatches": mism}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(out, open(args.out, "w"), indent=1)
