@@ -508,6 +508,19 @@ bool cold_path() {
   return on;
 }
 
+// largest launch the cold kernel takes (one 4-wave block per equation); above it the one-lane
+// ladder's throughput wins (tools/cold_sizes.py)
+#ifndef NWC_COLD_MAX
+#define NWC_COLD_MAX 3072
+#endif
+uint64_t cold_max() {
+  static const uint64_t m = [] {
+    const char* e = std::getenv("NWC_COLD_MAX");   // A/B
+    return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)NWC_COLD_MAX;
+  }();
+  return m;
+}
+
 // launch_verify flags: the caller checked on the host that every key is in the committee cache,
 // and/or out_words is already zero (both let the latency path run as a single kernel)
 constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4;   // LV_AUTO: the keys are in the auto cache
@@ -584,7 +597,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   // lane per new key) runs on the side stream beside the verification instead of after it
   // a small batch no cache covers (first-sight keys): one limb-sliced block per equation, the
   // batch leaf's torsion test inside it
-  const bool cold = half && !comb && !cm.n && n <= NWC_WIDE_MAX && cold_path();
+  const bool cold = half && !comb && !cm.n && n <= cold_max() && cold_path();
   const bool tors_beside = !strict && !comb && n <= NWC_WIDE_MAX && !cold;
   if (tors_beside) {
     HIP_TRY(hipEventRecord(d.ev_fork, s));

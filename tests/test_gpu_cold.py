@@ -1,5 +1,5 @@
 """GPU parity of the cold kernel (narwhal_amd/csrc/kernels.hip, k_verify_cold): calls of at most
-NWC_WIDE_MAX (1024) equations whose keys no cache holds run one limb-sliced block per equation,
+NWC_COLD_MAX (3072) equations whose keys no cache holds run one limb-sliced block per equation,
 with the batch leaf's torsion test (l A = [2^252] A + [l - 2^252] A) inside the same block.  Every
 golden verify case (torsion keys, small-order A and R, non-canonical encodings, s >= l) goes
 through it in both modes against the fixture's `strict` / `leaf` verdicts, and random triples with
@@ -27,7 +27,7 @@ def test_cold_golden_cases(golden_verify):
     arr = lambda k: np.stack([np.frombuffer(bytes.fromhex(c[k]), np.uint8) for c in cases])  # noqa: E731
     m, p, s = arr("msg"), arr("pk"), arr("sig")
     rng = np.random.default_rng(11)
-    for n in (1, 3, 64, 1000):
+    for n in (1, 3, 64, 1000, 3000):
         idx = rng.integers(0, len(cases), n) if n < len(cases) else np.resize(rng.permutation(len(cases)), n)
         for strict in (True, False):
             got = _verify(m[idx], p[idx], s[idx], strict)
