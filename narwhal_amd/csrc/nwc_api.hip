@@ -167,6 +167,10 @@ struct DevCtx {
   uint32_t ak_n = 0, ak_cap = 0, ak_slot_cap = 0;
   KeyIndex ak_host;                       // host copy of the auto cache's lookup table
   std::unordered_set<std::string> ak_seen;   // keys seen once (32-byte strings), bounded
+  // copy sources of the last auto-cache build, alive until the stream has passed it
+  std::vector<nwc::u32> ak_pend_keys;
+  std::vector<int32_t> ak_pend_slots;
+  bool ak_pending = false;
   std::mutex mu;
 
   int ensure_pinned(size_t bytes) {
@@ -333,7 +337,8 @@ constexpr size_t AUTO_SEEN_MAX = 4096;   // keys remembered as seen once (cleare
 // Keys of a small host call that missed every cache: a key seen before is added to the auto
 // cache (flags, 129-entry table and comb built on d.stream after this call's work; the next call
 // on this device is ordered after the build), a new one is remembered as seen.  The host copy
-// is updated only after the build is enqueued.  Caller holds d.mu and has set the device.
+// is updated once the build is enqueued; the call does not wait for it (its copy sources stay
+// in d.ak_pend_* until the next build has synchronised).  Caller holds d.mu and has set the device.
 int auto_insert(DevCtx& d, const uint8_t* pks, uint64_t n) {
   const uint32_t cap = auto_keys_cap();
   if (cap == 0 || d.ak_n >= cap) return 0;
@@ -355,6 +360,10 @@ int auto_insert(DevCtx& d, const uint8_t* pks, uint64_t n) {
   }
   const uint32_t m = (uint32_t)(add.size() / 8);
   if (m == 0) return 0;
+  if (d.ak_pending) {
+    HIP_TRY(hipStreamSynchronize(d.stream));   // the previous build's copy sources are free again
+    d.ak_pending = false;
+  }
   const uint32_t n0 = d.ak_n, n1 = n0 + m;
   if (n1 > d.ak_cap) {
     // grow (doubling, at most the configured capacity): copy what is built, free the old arrays
@@ -393,14 +402,16 @@ int auto_insert(DevCtx& d, const uint8_t* pks, uint64_t n) {
     HIP_TRY(hipMalloc(&d.ak_slots, 4 * (size_t)slots));
     d.ak_slot_cap = slots;
   }
-  HIP_TRY(hipMemcpyAsync(d.ak_keys + 8 * (size_t)n0, add.data(), 32 * (size_t)m, hipMemcpyHostToDevice, d.stream));
+  d.ak_pend_keys = std::move(add);
+  d.ak_pend_slots = table;
+  HIP_TRY(hipMemcpyAsync(d.ak_keys + 8 * (size_t)n0, d.ak_pend_keys.data(), 32 * (size_t)m, hipMemcpyHostToDevice,
+                         d.stream));
   hipLaunchKernelGGL(nwc::k_build_key_tables, dim3((unsigned)((m * 129 + 255) / 256)), dim3(256), 0, d.stream,
                      d.ak_keys + 8 * (size_t)n0, m, d.ak_tables + (size_t)n0 * 129, d.ak_flags + n0);
   HIP_TRY(hipGetLastError());
   if (int rc = build_key_combs(d, d.ak_keys + 8 * (size_t)n0, m, d.ak_comb + (size_t)n0 * nwc::COMB_PER_KEY)) return rc;
-  HIP_TRY(hipMemcpyAsync(d.ak_slots, table.data(), 4 * (size_t)slots, hipMemcpyHostToDevice, d.stream));
-  // synchronous: the host vectors above are the copy sources
-  HIP_TRY(hipStreamSynchronize(d.stream));
+  HIP_TRY(hipMemcpyAsync(d.ak_slots, d.ak_pend_slots.data(), 4 * (size_t)slots, hipMemcpyHostToDevice, d.stream));
+  d.ak_pending = true;
   next.slots = std::move(table);
   next.mask = slots - 1;
   d.ak_host = std::move(next);
