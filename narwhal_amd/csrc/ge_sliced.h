@@ -107,6 +107,8 @@ FES_DEV bool gs_is_identity(const gs_p2& p) {
 // map; the sign of x drops out), RFC 7748's x-only doubling (t1 = (U + W)^2, t2 = (U - W)^2,
 // U' = t1 t2, W' = (t1 - t2)(t2 + 121666 (t1 - t2))), two layers per doubling.  Projective
 // (U : W); the identity is (U : 0).  No square root: it can start before P is decompressed.
+// y must be tight (fe_tighten): U - W = 2y feeds fes_mul, whose odd-limb bound 2y exceeds for
+// raw fe_from_words limbs (tools/microbench/sliced_points.hip checks both against the doublings).
 FES_DEV void gs_xonly_dbl_n(fes y, int n, fes& U, fes& W) {
   U = fes_add_small(y, 1);
   W = fes_add_small(fes_neg(y), 1);

@@ -77,6 +77,32 @@ __global__ void k_check(unsigned* out) {
   }
 }
 
+// x-only chain (gs_xonly_dbl_n) vs Edwards doublings: u([2^k] P) == (Z + Y) / (Z - Y) of the
+// per-lane [2^k] P, for k = 1, 7 and 252, cross-multiplied; out[w] = number of mismatches
+__global__ void k_xonly_check(unsigned* out) {
+  const int w = blockIdx.x;
+  ge_p3 P = base_point();
+  const ge_cached bc = ge_p3_to_cached(P);
+  for (int k = 0; k < 1 + w; ++k) P = ge_p1p1_to_p3(ge_add_cached(P, bc));
+  if (w & 1) { P.X = fe_neg(P.X); P.Y = fe_neg(P.Y); }   // odd waves: P + T2 (a torsion component)
+  // affine y of P
+  u32 aw[16];
+  affine_words(P.X, P.Y, P.Z, aw);
+  const fe y = fe_tighten(fe_from_words(aw + 8));   // as in k_verify_cold (fes_mul input bounds)
+  unsigned bad = 0;
+  const int ks[3] = {1, 7, 252};
+  for (int j = 0; j < 3; ++j) {
+    fes U, W;
+    gs_xonly_dbl_n(fes_from_fe(y), ks[j], U, W);
+    ge_p2 q = ge_p3_to_p2(P);
+    for (int k = 0; k < ks[j]; ++k) q = ge_p1p1_to_p2(ge_p2_dbl(q));
+    const fe lhs = fe_mul(fe_from_fes(U), fe_sub(q.Z, q.Y));
+    const fe rhs = fe_mul(fe_from_fes(W), fe_add(q.Z, q.Y));
+    bad += fe_is_zero(fe_sub(lhs, rhs)) ? 0u : 1u;
+  }
+  if (threadIdx.x == 0) out[w] = bad;
+}
+
 __global__ void k_tors_lane(const ge_p3* P, unsigned* out) {
   if (threadIdx.x == 0) out[0] = ge_has_torsion(P[0]);
 }
@@ -103,6 +129,14 @@ int main() {
     bad_tors += (h[6 * w + 2] != 0) + (h[6 * w + 3] != 0) + (h[6 * w + 4] != 1) + (h[6 * w + 5] != 1);
   }
   printf("points %d: dbl mismatches %d, add mismatches %d, torsion-test errors %d\n", W, bad_dbl, bad_add, bad_tors);
+  hipLaunchKernelGGL(k_xonly_check, dim3(W), dim3(64), 0, 0, d);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(h.data(), d, W * 4, hipMemcpyDeviceToHost));
+  int bad_x = 0;
+  for (int w = 0; w < W; ++w) bad_x += h[w];
+  printf("x-only u([2^k] P) vs Edwards doublings (k = 1, 7, 252; half the points with torsion): %d mismatches of %d\n",
+         bad_x, 3 * W);
+  bad_tors += bad_x;
   ge_p3* P;
   CHECK(hipMalloc(&P, sizeof(ge_p3)));
   hipLaunchKernelGGL(k_one_point, dim3(1), dim3(64), 0, 0, P);
