@@ -80,6 +80,32 @@ int nwc_set_committee(const uint8_t* pks, size_t n);
  * Diagnostics only: verdicts never depend on either cache.  Not part of the crate's API. */
 int nwc_cache_stats(uint32_t* committee_keys, uint32_t* auto_keys);
 
+/* Auto key cache lifecycle of the calling thread's device: capacity (NWC_AUTO_KEYS), insert
+ * batches built so far, and calls served by the latency kernel over it.  Once full, new keys
+ * replace the oldest (FIFO); nwc_set_committee empties it.  Any pointer may be NULL.
+ * Diagnostics only, not part of the crate's API. */
+int nwc_auto_cache_info(uint32_t* capacity, uint64_t* builds, uint64_t* hits);
+
+/* ---- worker batch digests behind a Processor-shaped queue (worker/src/processor.rs:35-55) ----
+ * Replaces the Processor's per-batch `Sha512::digest(&batch)[..32]` (:38) for workers that can
+ * hand batches over in groups.  A digester owns a drain thread on the calling thread's device
+ * (nwc_dev_set_device): it takes the first submitted batch, then whatever else arrives within
+ * max_wait_us (up to max_group batches), and digests the group with one GPU launch on its own
+ * stream.  Batches are BORROWED: the caller keeps each one alive until its digest has been
+ * polled (the Processor stores the batch after hashing it anyway).  Digests come back in
+ * submission order with the caller's tag.  One 500-KB batch alone takes ~30 ms on the GPU (a
+ * sequential SHA-512 chain on one lane) against ~0.36 ms on one host core: the GPU pays only for
+ * groups of ~1,000+ batches.  create returns NULL on failure
+ * (nwc_last_error); poll waits up to wait_us for at least one digest and reports a device error
+ * of the drain thread (sticky); destroy digests what is queued, then frees the digester. */
+typedef struct nwc_digester nwc_digester;
+nwc_digester* nwc_digester_create(uint32_t max_group, uint32_t max_wait_us);
+int nwc_digester_submit(nwc_digester* q, const uint8_t* batch, size_t len, uint64_t tag);
+int nwc_digester_poll(nwc_digester* q, size_t max, uint32_t wait_us, uint64_t* tags, uint8_t* digests32,
+                      size_t* n_done);
+int nwc_digester_stats(nwc_digester* q, uint64_t* groups, uint64_t* batches, uint64_t* bytes);
+int nwc_digester_destroy(nwc_digester* q);
+
 /* ---- primary messages ---------------------------------------- */
 /* config::Committee for the message checks (config/src/lib.rs:134-212): n authorities with
  * their keys, stakes (Committee::stake) and worker ids (Committee::worker): authority k runs
@@ -141,6 +167,19 @@ int nwc_dev_verify(const void* d_msgs, const void* d_msg_index, uint64_t msg_str
 /* Per-certificate AND of leaf verdict words (d_offsets: device u32[m+1]). */
 int nwc_dev_cert_reduce(const void* d_leaf_words, const void* d_offsets, uint64_t m, uint64_t nvotes,
                         void* d_cert_words, void* d_bad_words, void* stream);
+/* Signature::verify_batch over m certificates as dalek's own batch equation (crypto/src/lib.rs:
+ * 206-219; ed25519-dalek 1.0.1 batch.rs): per certificate, sum z_i R_i + sum (z_i k_i mod l) A_i -
+ * (sum z_i s_i mod l) B == O with random 128-bit z_i, one Straus pass with shared doublings
+ * (k_verify_straus); the votes of certificates it rejects are then re-decided by the exact
+ * per-vote leaves, so d_leaf_words (a bit per vote, as nwc_dev_verify's) feeds nwc_dev_cert_reduce
+ * for the certificate verdicts and the exact bad-vote set.  d_offsets: m + 1 uint32 vote offsets;
+ * d_msg_index: the certificate of each vote.  Same verdicts as the leaf path on the deterministic
+ * domain; on dalek's randomized domain (pure-torsion residuals, torsion-bearing keys) a
+ * certificate passes with dalek's probability (~1/ord) where the leaf path answers Err.  Without
+ * the basepoint comb (NWC_COMB16=0) or for certificates of > 1,536 votes it runs the leaves. */
+int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, const void* d_msg_index, uint64_t m,
+                                uint64_t nvotes, const void* d_pks, const void* d_sigs, void* d_leaf_words,
+                                void* stream);
 int nwc_dev_sha512_trunc32(const void* d_data, const void* d_offsets, uint64_t n, void* d_out32,
                            void* stream);
 /* Same, message i = d_data[d_starts[i] .. d_ends[i]) (device u64 arrays): any layout, e.g. a

@@ -36,6 +36,7 @@ _SIGS = {
     "nwc_verify_batch_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p, _c_u8p]),
     "nwc_set_committee": (ctypes.c_int, [_c_u8p, ctypes.c_size_t]),
     "nwc_cache_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "nwc_auto_cache_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_digest32": (ctypes.c_int, [_c_u8p, ctypes.c_size_t, _c_u8p]),
     "nwc_sha512_trunc32_many": (ctypes.c_int, [_c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p]),
     "nwc_dev_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -43,6 +44,9 @@ _SIGS = {
                                       ctypes.c_void_p]),
     "nwc_dev_cert_reduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "nwc_dev_verify_batch_straus": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p]),
     "nwc_dev_sha512_trunc32": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                               ctypes.c_void_p]),
     "nwc_dev_sha512_trunc32_ranges": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -58,6 +62,12 @@ _SIGS = {
                                                  ctypes.c_void_p]),
     "nwc_sanitize_messages": (ctypes.c_int, [_c_u8p, _c_u8p, ctypes.c_size_t, ctypes.c_uint64, _c_u8p, _c_u8p,
                                              _c_u8p, _c_u8p]),
+    "nwc_digester_create": (ctypes.c_void_p, [ctypes.c_uint32, ctypes.c_uint32]),
+    "nwc_digester_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]),
+    "nwc_digester_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]),
+    "nwc_digester_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "nwc_digester_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "nwc_shard_bounds": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "nwc_cert_cuts": (ctypes.c_int, [_c_u8p, ctypes.c_size_t, ctypes.c_uint32, _c_u8p]),
@@ -85,6 +95,8 @@ def load(init: bool = True, device_mask: int = 0):
                                   % LIB_PATH)
             lib = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in _SIGS.items():
+                if os.environ.get("NWC_LIB_PATH") and not hasattr(lib, name):
+                    continue   # an A/B build from before this entry point existed
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args

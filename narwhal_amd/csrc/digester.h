@@ -1,0 +1,266 @@
+// The worker's batch digests behind a Processor-shaped queue (worker/src/processor.rs:35-55).
+//
+// The reference's Processor task takes one batch off its channel, hashes it
+// (`Sha512::digest(&batch)[..32]`, :38), stores it and sends the digest on.  A GPU digest only pays
+// for many batches at once (one batch is a 3,970-block chain on one lane, ~30 ms), so
+// the device-side Processor drains its channel instead: a drain thread takes the first batch, then
+// whatever else arrives within `max_wait_us` (up to `max_group` batches), and digests the group with
+// one launch.  Results come back in submission order.
+//
+// Data path per group: the borrowed batches are gathered into two pinned 64-MB stages in turn
+// (16-byte-aligned starts, the kernel's dwordx4 path) and copied on the digester's own stream into
+// one device buffer while the next stage is filled; then k_sha512_digest32[_sched] over the group
+// and one D2H of 32 bytes per batch.  The digester has its own stream and buffers (it does not
+// serialise with verification calls on the device's context).  Included by nwc_api.hip.
+#pragma once
+#include <array>
+#include <condition_variable>
+#include <deque>
+
+namespace {
+
+struct Digester {
+  struct Item { const uint8_t* p; size_t len; uint64_t tag; };
+  uint32_t max_group, max_wait_us;
+  int hip_id;
+  std::mutex mu;
+  std::condition_variable cv_in, cv_out;
+  std::deque<Item> in;
+  std::deque<Item> out;            // tag + digest (p unused)
+  std::deque<std::array<uint8_t, 32>> out_dig;
+  int err = 0;
+  std::string err_msg;
+  bool stop = false;
+  uint64_t groups = 0, batches = 0, bytes = 0;
+  std::thread th;
+  // device side (touched by the drain thread only)
+  hipStream_t stream = nullptr;
+  static constexpr size_t STAGE = 64u << 20;
+  uint8_t* stage[2] = {nullptr, nullptr};
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  uint8_t* ddata = nullptr;
+  size_t ddata_cap = 0;
+  uint64_t* dse = nullptr;        // starts then ends
+  uint8_t* dout = nullptr;
+  size_t k_cap = 0;
+  uint64_t* hse = nullptr;        // pinned starts/ends
+  uint8_t* hout = nullptr;        // pinned digests
+
+  int init() {
+    HIP_TRY(hipSetDevice(hip_id));
+    HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    for (int s = 0; s < 2; ++s) {
+      HIP_TRY(hipHostMalloc(&stage[s], STAGE, hipHostMallocDefault));
+      HIP_TRY(hipEventCreateWithFlags(&stage_ev[s], hipEventDisableTiming));
+    }
+    return 0;
+  }
+  void release() {
+    (void)hipSetDevice(hip_id);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (int s = 0; s < 2; ++s) {
+      if (stage[s]) (void)hipHostFree(stage[s]);
+      if (stage_ev[s]) (void)hipEventDestroy(stage_ev[s]);
+    }
+    if (ddata) (void)hipFree(ddata);
+    if (dse) (void)hipFree(dse);
+    if (dout) (void)hipFree(dout);
+    if (hse) (void)hipHostFree(hse);
+    if (hout) (void)hipHostFree(hout);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  // SHA-512[..32] of every batch of the group into out32 (32 bytes each)
+  int digest_group(const std::vector<Item>& g, uint8_t* out32) {
+    const size_t k = g.size();
+    if (k > k_cap) {
+      const size_t nk = std::max(k, 2 * k_cap);
+      if (dse) HIP_TRY(hipFree(dse));
+      if (dout) HIP_TRY(hipFree(dout));
+      if (hse) HIP_TRY(hipHostFree(hse));
+      if (hout) HIP_TRY(hipHostFree(hout));
+      dse = nullptr; dout = nullptr; hse = nullptr; hout = nullptr; k_cap = 0;
+      HIP_TRY(hipMalloc(&dse, 16 * nk));
+      HIP_TRY(hipMalloc(&dout, 32 * nk));
+      HIP_TRY(hipHostMalloc(&hse, 16 * nk, hipHostMallocDefault));
+      HIP_TRY(hipHostMalloc(&hout, 32 * nk, hipHostMallocDefault));
+      k_cap = nk;
+    }
+    uint64_t total = 0;
+    for (size_t i = 0; i < k; ++i) {
+      hse[i] = total;
+      hse[k + i] = total + g[i].len;
+      total += (g[i].len + 15) & ~(uint64_t)15;
+    }
+    if (total + 16 > ddata_cap) {
+      if (ddata) HIP_TRY(hipFree(ddata));
+      ddata = nullptr;
+      ddata_cap = 0;
+      const size_t cap = (total + 16) + (total + 16) / 4;
+      HIP_TRY(hipMalloc(&ddata, cap));
+      ddata_cap = cap;
+    }
+    // gather through the two pinned stages: fill one while the other's copy is in flight
+    int s = 0;
+    size_t fill = 0;
+    uint64_t dst = 0;   // device offset of the stage's first byte
+    bool used[2] = {false, false};
+    auto flush = [&]() -> int {
+      if (fill == 0) return 0;
+      HIP_TRY(hipMemcpyAsync(ddata + dst, stage[s], fill, hipMemcpyHostToDevice, stream));
+      HIP_TRY(hipEventRecord(stage_ev[s], stream));
+      used[s] = true;
+      dst += fill;
+      fill = 0;
+      s ^= 1;
+      if (used[s]) HIP_TRY(hipEventSynchronize(stage_ev[s]));   // its previous copy has landed
+      return 0;
+    };
+    for (size_t i = 0; i < k; ++i) {
+      const uint8_t* p = g[i].p;
+      size_t left = g[i].len;
+      const size_t padded = (g[i].len + 15) & ~(size_t)15;
+      size_t pad = padded - g[i].len;
+      while (left) {
+        const size_t c = std::min(left, STAGE - fill);
+        std::memcpy(stage[s] + fill, p, c);
+        fill += c; p += c; left -= c;
+        if (fill == STAGE) if (int rc = flush()) return rc;
+      }
+      while (pad) {   // alignment gap (never read by the kernel)
+        const size_t c = std::min(pad, STAGE - fill);
+        fill += c; pad -= c;
+        if (fill == STAGE) if (int rc = flush()) return rc;
+      }
+    }
+    if (int rc = flush()) return rc;
+    HIP_TRY(hipMemcpyAsync(dse, hse, 16 * k, hipMemcpyHostToDevice, stream));
+    if (int rc = launch_digest(ddata, dse, dse + k, k, dout, stream)) return rc;
+    HIP_TRY(hipMemcpyAsync(hout, dout, 32 * k, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    std::memcpy(out32, hout, 32 * k);
+    return 0;
+  }
+
+  void run() {
+    (void)hipSetDevice(hip_id);
+    std::vector<Item> g;
+    std::vector<uint8_t> dig;
+    for (;;) {
+      g.clear();
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_in.wait(lk, [&] { return stop || !in.empty(); });
+        if (in.empty()) return;   // stop, drained
+        g.push_back(in.front());
+        in.pop_front();
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
+        while (g.size() < max_group) {
+          if (in.empty()) {
+            if (stop || max_wait_us == 0) break;
+            if (!cv_in.wait_until(lk, deadline, [&] { return stop || !in.empty(); })) break;
+            if (in.empty()) break;
+          }
+          g.push_back(in.front());
+          in.pop_front();
+        }
+      }
+      dig.resize(32 * g.size());
+      const int rc = digest_group(g, dig.data());
+      std::lock_guard<std::mutex> lk(mu);
+      if (rc) {
+        if (!err) { err = rc; err_msg = t_err; }
+      } else {
+        ++groups;
+        for (size_t i = 0; i < g.size(); ++i) {
+          out.push_back(Item{nullptr, g[i].len, g[i].tag});
+          std::array<uint8_t, 32> a;
+          std::memcpy(a.data(), dig.data() + 32 * i, 32);
+          out_dig.push_back(a);
+          ++batches;
+          bytes += g[i].len;
+        }
+      }
+      cv_out.notify_all();
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+nwc_digester* nwc_digester_create(uint32_t max_group, uint32_t max_wait_us) {
+  if (require_init()) return nullptr;
+  if (max_group == 0) { set_err(NWC_ERR_ARG, "max_group must be >= 1"); return nullptr; }
+  auto* q = new Digester();
+  q->max_group = max_group;
+  q->max_wait_us = max_wait_us;
+  q->hip_id = ctx(t_dev < (int)g_devs.size() ? t_dev : 0)->hip_id;
+  if (q->init()) {
+    q->release();
+    delete q;
+    return nullptr;
+  }
+  q->th = std::thread([q] { q->run(); });
+  return reinterpret_cast<nwc_digester*>(q);
+}
+
+int nwc_digester_submit(nwc_digester* h, const uint8_t* batch, size_t len, uint64_t tag) {
+  auto* q = reinterpret_cast<Digester*>(h);
+  if (!q) return set_err(NWC_ERR_ARG, "null digester");
+  if (len && !batch) return set_err(NWC_ERR_ARG, "null batch");
+  {
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (q->stop) return set_err(NWC_ERR_ARG, "digester is shutting down");
+    q->in.push_back(Digester::Item{batch, len, tag});
+  }
+  q->cv_in.notify_one();
+  return 0;
+}
+
+int nwc_digester_poll(nwc_digester* h, size_t max, uint32_t wait_us, uint64_t* tags, uint8_t* digests32, size_t* n_done) {
+  auto* q = reinterpret_cast<Digester*>(h);
+  if (!q || !n_done || (max && (!tags || !digests32))) return set_err(NWC_ERR_ARG, "null argument");
+  std::unique_lock<std::mutex> lk(q->mu);
+  if (wait_us && q->out.empty() && !q->err)
+    q->cv_out.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return !q->out.empty() || q->err; });
+  size_t n = 0;
+  while (n < max && !q->out.empty()) {
+    tags[n] = q->out.front().tag;
+    std::memcpy(digests32 + 32 * n, q->out_dig.front().data(), 32);
+    q->out.pop_front();
+    q->out_dig.pop_front();
+    ++n;
+  }
+  *n_done = n;
+  if (q->err) return set_err(q->err, "%s", q->err_msg.c_str());
+  return 0;
+}
+
+int nwc_digester_stats(nwc_digester* h, uint64_t* groups, uint64_t* batches, uint64_t* bytes) {
+  auto* q = reinterpret_cast<Digester*>(h);
+  if (!q) return set_err(NWC_ERR_ARG, "null digester");
+  std::lock_guard<std::mutex> lk(q->mu);
+  if (groups) *groups = q->groups;
+  if (batches) *batches = q->batches;
+  if (bytes) *bytes = q->bytes;
+  return 0;
+}
+
+int nwc_digester_destroy(nwc_digester* h) {
+  auto* q = reinterpret_cast<Digester*>(h);
+  if (!q) return 0;
+  {
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->stop = true;
+  }
+  q->cv_in.notify_all();
+  if (q->th.joinable()) q->th.join();
+  const int rc = q->err;
+  q->release();
+  delete q;
+  return rc;
+}
+
+}  // extern "C"

@@ -180,6 +180,14 @@ FE_DEV void ge_decompressN(ge_p3 out[N], const u32* const w[N], u32 ycanon[N][8]
   _Pragma("unroll") for (int k = 0; k < N; ++k) ge_decompress_finish(w[k], y[k], u[k], v[k], b[k], out[k], ycanon[k], ok[k]);
 }
 
+// One encoding, no pointer indirection (for inlined call sites whose input words live in VGPRs).
+FE_DEV void ge_decompress1(const u32 w[8], ge_p3& out, u32 ycanon[8], bool& ok) {
+  fe y, u, v3, z;
+  ge_decompress_prep(w, y, u, v3, z);
+  const fe b = fe_pow22523(z);
+  ge_decompress_finish(w, y, u, v3, b, out, ycanon, ok);
+}
+
 // A decompressed point is small-order iff its y is one of the five y-coordinates of E[8]
 // (0, 1, -1, +-y8): every such y decodes, and E[8] has exactly these y values.  Equivalent
 // to dalek's `mul_by_cofactor().is_identity()` for decoded points.

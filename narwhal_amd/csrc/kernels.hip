@@ -41,6 +41,17 @@
 #ifndef NWC_ADD_LT_SPLIT
 #define NWC_ADD_LT_SPLIT 1
 #endif
+//   NWC_PROLOGUE_LOOP     uncached half-size path: scalars first, then R and A decoded in a rolled
+//                         two-iteration loop, each table written at once (1); or both points
+//                         decoded by a noinline call and held through scratch memory (0, round 2)
+#ifndef NWC_PROLOGUE_LOOP
+#define NWC_PROLOGUE_LOOP 0
+#endif
+//   NWC_PACKED_TABLES     per-lane ladder tables with 128-B entries (limbs packed, one cache line
+//                         per gather) (1) or 160-B entries of plain limbs (0)
+#ifndef NWC_PACKED_TABLES
+#define NWC_PACKED_TABLES 1
+#endif
 
 namespace nwc {
 
@@ -378,11 +389,78 @@ __global__ void k_build_comb16(ge_niels_pad* __restrict__ out, const ge_p3* __re
 // so a wave touches ~128 lines per lookup instead of the whole wave's table (the compiler's
 // private memory interleaves lanes dword by dword).
 constexpr int TAB_ENTRIES = 9;
+#if NWC_PACKED_TABLES
+// Packed entries: each coordinate's ten limbs, made non-negative, in 32 bytes (fields of 26, 26,
+// 26, 25, 26, 25, 26, 25, 26, 25 bits at bit offsets 0, 26, 52, 78, 103, 129, 154, 180, 205, 231;
+// limb 1 keeps one slack bit for the final carry).  An entry is 128 B on a 128-B boundary, so a
+// gather of one entry touches exactly one cache line (160-B entries touch two).
+constexpr int TAB_U4_PER_ENTRY = 8;
+
+// f (limbs |f_i| < 2^26.5 even / 2^25.5 odd: sums of two tight elements) + 2p, floor-carried to
+// limbs in [0, 2^26) / [0, 2^25) (limb 1 < 2^25 + 2), packed into two uint4.
+__device__ __forceinline__ void fe_pack(const fe& f, uint4& lo, uint4& hi) {
+  u32 h[10];
+  i32 c = 0;
+  _Pragma("unroll") for (int i = 0; i < 10; ++i) {
+    const int w = (i & 1) ? 25 : 26;
+    const i32 bias = i == 0 ? 2 * ((1 << 26) - 19) : 2 * ((1 << w) - 1);
+    const i32 v = f.v[i] + bias + c;   // > 0
+    c = v >> w;
+    h[i] = (u32)v & ((1u << w) - 1u);
+  }
+  h[0] += 19u * (u32)c;                // c <= 3: h[0] < 2^26 + 57
+  h[1] += h[0] >> 26;
+  h[0] &= (1u << 26) - 1u;
+  lo.x = h[0] | (h[1] << 26);
+  lo.y = (h[1] >> 6) | (h[2] << 20);
+  lo.z = (h[2] >> 12) | (h[3] << 14);
+  lo.w = (h[3] >> 18) | (h[4] << 7);
+  hi.x = (h[4] >> 25) | (h[5] << 1) | (h[6] << 26);
+  hi.y = (h[6] >> 6) | (h[7] << 20);
+  hi.z = (h[7] >> 12) | (h[8] << 13);
+  hi.w = (h[8] >> 19) | (h[9] << 7);
+}
+// Unpacked limbs are in [0, 2^26) / [0, 2^25 + 2): within the multiplier's loose input bound
+// (including the 19x on the right operand).
+__device__ __forceinline__ fe fe_unpack(const uint4& lo, const uint4& hi) {
+  constexpr u32 M26 = (1u << 26) - 1u, M25 = (1u << 25) - 1u;
+  fe r;
+  r.v[0] = (i32)(lo.x & M26);
+  r.v[1] = (i32)(__builtin_amdgcn_alignbit(lo.y, lo.x, 26) & M26);
+  r.v[2] = (i32)(__builtin_amdgcn_alignbit(lo.z, lo.y, 20) & M26);
+  r.v[3] = (i32)(__builtin_amdgcn_alignbit(lo.w, lo.z, 14) & M25);
+  r.v[4] = (i32)(__builtin_amdgcn_alignbit(hi.x, lo.w, 7) & M26);
+  r.v[5] = (i32)((hi.x >> 1) & M25);
+  r.v[6] = (i32)(__builtin_amdgcn_alignbit(hi.y, hi.x, 26) & M26);
+  r.v[7] = (i32)(__builtin_amdgcn_alignbit(hi.z, hi.y, 20) & M25);
+  r.v[8] = (i32)(__builtin_amdgcn_alignbit(hi.w, hi.z, 13) & M26);
+  r.v[9] = (i32)(hi.w >> 7);
+  return r;
+}
+#else
 constexpr int TAB_U4_PER_ENTRY = 10;
-constexpr size_t TAB_BYTES_PER_LANE = TAB_ENTRIES * TAB_U4_PER_ENTRY * 16;   // 1440
+#endif
+constexpr size_t TAB_BYTES_PER_LANE = TAB_ENTRIES * TAB_U4_PER_ENTRY * 16;   // 1440 (1152 packed)
 
 struct LaneTable {
   uint4* p;
+#if NWC_PACKED_TABLES
+  __device__ __forceinline__ void store(int e, const ge_cached& c) const {
+    const fe* co = &c.YpX;
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) {
+      uint4 lo, hi;
+      fe_pack(co[k], lo, hi);
+      p[e * 8 + 2 * k] = lo;
+      p[e * 8 + 2 * k + 1] = hi;
+    }
+  }
+  __device__ __forceinline__ ge_cached load(int e) const {
+    ge_cached c;
+    fe* co = &c.YpX;
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) co[k] = fe_unpack(p[e * 8 + 2 * k], p[e * 8 + 2 * k + 1]);
+    return c;
+  }
+#else
   __device__ __forceinline__ void store(int e, const ge_cached& c) const {
     const uint4* src = reinterpret_cast<const uint4*>(&c);
     _Pragma("unroll") for (int i = 0; i < TAB_U4_PER_ENTRY; ++i) p[e * TAB_U4_PER_ENTRY + i] = src[i];
@@ -393,11 +471,16 @@ struct LaneTable {
     _Pragma("unroll") for (int i = 0; i < TAB_U4_PER_ENTRY; ++i) dst[i] = p[e * TAB_U4_PER_ENTRY + i];
     return c;
   }
+#endif
 };
-static_assert(sizeof(ge_cached) == TAB_U4_PER_ENTRY * 16, "cached point layout");
+static_assert(NWC_PACKED_TABLES || sizeof(ge_cached) == TAB_U4_PER_ENTRY * 16, "cached point layout");
 
-// Coordinate k (0 YpX, 1 YmX, 2 Z, 3 T2d) of entry e: 40 bytes at an 8-byte-aligned offset.
+// Coordinate k (0 YpX, 1 YmX, 2 Z, 3 T2d) of entry e: 40 bytes at an 8-byte-aligned offset
+// (packed: 32 bytes at a 32-byte-aligned offset).
 __device__ __forceinline__ fe lt_load_fe(const LaneTable& tab, int e, int k) {
+#if NWC_PACKED_TABLES
+  return fe_unpack(tab.p[e * 8 + 2 * k], tab.p[e * 8 + 2 * k + 1]);
+#else
   const uint2* q = reinterpret_cast<const uint2*>(tab.p) + e * 20 + k * 5;
   fe r;
   _Pragma("unroll") for (int i = 0; i < 5; ++i) {
@@ -406,6 +489,19 @@ __device__ __forceinline__ fe lt_load_fe(const LaneTable& tab, int e, int k) {
     r.v[2 * i + 1] = (i32)v.y;
   }
   return r;
+#endif
+}
+// The ladder's first entry as a completed point: the table's coordinates re-centred first when
+// packed (2Z of limbs up to 2^27 would exceed the multiplier's right-operand bound).
+__device__ __forceinline__ ge_cached lt_first(const LaneTable& tab, int e) {
+  ge_cached c = tab.load(e);
+#if NWC_PACKED_TABLES
+  c.YpX = fe_tighten(c.YpX);
+  c.YmX = fe_tighten(c.YmX);
+  c.Z = fe_tighten(c.Z);
+  c.T2d = fe_tighten(c.T2d);
+#endif
+  return c;
 }
 
 // t + (neg ? -q : q) for q = tab[e], t completed (p1p1), result completed: 8M, with the entry
@@ -736,7 +832,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
   i32 da = cd.top, dr = dd.top;   // top digits are >= 0
 #if NWC_LADDER_PREFETCH
   ge_cached ea = ta.load(da), er = tr.load(dr);
-  ge_p1p1 t = ge_cached_to_p1p1(ea);
+  ge_p1p1 t = ge_cached_to_p1p1(lt_first(ta, da));
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     if (w != W - 1) ladder_dbl4(t);
@@ -759,7 +855,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
   // parked in LDS (BaseDigits), so the loop carries only the accumulator and a few scalars
   park16(bd, BD_C, cd);
   park16(bd, BD_D, dd);
-  ge_p1p1 t = ge_cached_to_p1p1(ta.load(da));
+  ge_p1p1 t = ge_cached_to_p1p1(lt_first(ta, da));
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     i32 d0 = 0, d1 = 0;
@@ -784,6 +880,27 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
   return ge_p1p1_to_p2(t);
 }
 
+// The same ladder over digit strings already parked in LDS (BD_C, BD_D; top digits passed in).
+__device__ __forceinline__ ge_p2 half_scalarmult_parked(const LaneTable& ta, const LaneTable& tr, i32 c_top, i32 d_top,
+                                                        BaseDigits bd, const ge_niels_pad* T24, uint4* stage, int W) {
+  i32 da = c_top, dr = d_top;   // top digits are >= 0
+  ge_p1p1 t = ge_cached_to_p1p1(lt_first(ta, da));
+#pragma unroll 1
+  for (int w = W - 1; w >= 0; --w) {
+    i32 d0 = 0, d1 = 0;
+    const int nb = base_fetch(w, bd, d0, d1, T24, stage);
+    if (w != W - 1) {
+      ladder_dbl4(t);
+      da = digit16(bd, BD_C, w, W);
+      t = add_lt(t, ta, da < 0 ? -da : da, da < 0);
+      dr = digit16(bd, BD_D, w, W);
+    }
+    t = add_lt(t, tr, dr < 0 ? -dr : dr, dr < 0);
+    base_adds(t, nb, d0, d1, stage, T24);
+  }
+  return ge_p1p1_to_p2(t);
+}
+
 // Half-size ladder with a cached key: Q = eB*B + c'*(-A) + d*(-R) where the A term uses the key's
 // radix-256 Niels table (one add at every even window, no per-equation table or decompression).
 // ca: radix-256 digits of |c| starting at window (W-1) & ~1; c_neg flips every A entry.
@@ -792,7 +909,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Dig
                                                         const ge_niels_pad* T24, uint4* stage, int W) {
   i32 dr = dd.top;   // >= 0
   ge_cached er = tr.load(dr);
-  ge_p1p1 t = ge_cached_to_p1p1(er);
+  ge_p1p1 t = ge_cached_to_p1p1(lt_first(tr, dr));
   i32 dA = next256(ca);
   ge_niels ean = key_tab[dA < 0 ? -dA : dA];
 #pragma unroll 1
@@ -953,6 +1070,67 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
     const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
     return ok && ident && h.ok;
   }
+#if NWC_PROLOGUE_LOOP
+  // Scalars first (challenge, lattice reduction, digit strings parked in LDS), then one rolled
+  // two-iteration loop decodes R and A in turn and writes each point's table at once: one point
+  // is live at a time, the decompression is inlined once (no call frame, no points passed through
+  // scratch memory), and nothing but the accumulator and two top digits reaches the ladder.
+  u32 sw[8];
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) sw[i] = sigw[8 + i];
+  bool ok = sc_lt_l(sw);
+  u32 kw[8];
+  challenge(sigw, aw, mw, kw);
+  const lat::HalfScalars h = lat::reduce(kw);
+  const int W = max(wave_windows(h.ok ? h.bits : 0), min(force_w, HALF_WINDOWS_MAX));
+  fallback = !h.ok;
+  {
+    Digits24 el, eh;
+    base_digits(h.d, sw, el, eh);
+    base_digits_park(bd, el, eh);
+  }
+  i32 c_top, d_top;
+  {
+    const Digits16 cd = recode16(h.c, W), dd = recode16(h.d, W);
+    park16(bd, BD_C, cd);
+    park16(bd, BD_D, dd);
+    c_top = cd.top;
+    d_top = dd.top;
+  }
+  const bool c_neg = h.c_neg;
+#pragma unroll 1
+  for (int j = 0; j < 2; ++j) {
+    // j = 0: R (table of -R);  j = 1: A (table of -c A / |c| = c < 0 ? A : -A)
+    u32 in[8];
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) in[i] = j ? aw[i] : sigw[i];
+    ge_p3 P;
+    u32 yc[8];
+    bool dok;
+    ge_decompress1(in, P, yc, dok);
+    const bool small = strict && ycanon_is_small_order(yc);
+    ok = ok && dok && !small;
+    const bool neg = (j == 0) || !c_neg;
+    P.X = fe_select(P.X, fe_neg(P.X), neg);
+    P.T = fe_select(P.T, fe_neg(P.T), neg);
+#if NWC_PROLOGUE_LOOP == 2
+    // park the point as its table's entry 1; both tables are built after the second decompression,
+    // right before the ladder reads them (a table written ~30k instructions earlier is colder)
+    LaneTable{j ? ta.p : tr.p}.store(1, ge_p3_to_cached(P));
+#else
+    build_table(LaneTable{j ? ta.p : tr.p}, P);
+#endif
+  }
+#if NWC_PROLOGUE_LOOP == 2
+#pragma unroll 1
+  for (int j = 0; j < 2; ++j) {
+    const LaneTable tab{j ? ta.p : tr.p};
+    const ge_p3 P = ge_p1p1_to_p3(ge_cached_to_p1p1(lt_first(tab, 1)));
+    build_table(tab, P);
+  }
+#endif
+  const ge_p2 q = half_scalarmult_parked(ta, tr, c_top, d_top, bd, T24, stage, W);
+  const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
+  return ok && ident && h.ok;
+#else
   Prologue p;
   prologue<1>(p, mw, aw, sigw, strict);
   const lat::HalfScalars h = lat::reduce(p.kw);
@@ -970,6 +1148,7 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
   const ge_p2 q = half_scalarmult(ta, tr, cd, dd, bd, T24, stage, W);
   const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
   return p.ok && ident && h.ok;
+#endif
 }
 
 // ------------------------------------------------------------------------------- verify
@@ -2157,6 +2336,10 @@ __global__ __launch_bounds__(256) void k_keygen_sign(const uint8_t* __restrict__
   uint32_t* so = reinterpret_cast<uint32_t*>(sigs + 64 * i);
   _Pragma("unroll") for (int j = 0; j < 8; ++j) { po[j] = pk[j]; so[j] = R[j]; so[8 + j] = s[j]; }
 }
+
+}  // namespace nwc
+#include "straus.h"
+namespace nwc {
 
 // Seeds / messages of the synthetic workloads (SURVEY.md §8(d) cfg 2):
 //   out_i = SHA-512(tag || u64le(first + i))[..32]

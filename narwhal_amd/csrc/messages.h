@@ -327,9 +327,53 @@ __device__ __forceinline__ int dig_cmp(const u32 a[8], const u32 b[8]) {
 //   MAP (payload, 9 words): ascending digests, one entry per digest with the LAST wire value
 //        (serde's BTreeMap visitor inserts each entry; insert replaces an existing key's value).
 // Strictly ascending input -- what serialising a BTree* produces -- is copied as is.  Otherwise
-// entry e goes to its stable-sort rank (#smaller digests + #equal digests before it; cnt compares
-// per entry) and the sorted run is compacted in place 64 entries per step, keeping the first
-// (SET) or the last (MAP) of each run of equal digests.  Every lane of the wave must call this.
+// the entries are sorted by (digest, wire index) -- up to CANON_RANK_MAX entries by rank (entry e
+// goes to #smaller digests + #equal digests before it; cnt compares per entry), more by a bitonic
+// network in dst (O(cnt log^2 cnt), so a Byzantine header of a maximum frame's worth of unsorted
+// entries costs milliseconds, not the rank method's cnt^2 loads) -- and the sorted run is compacted
+// in place 64 entries per step, keeping the first (SET) or the last (MAP) of each run of equal
+// digests.  Every lane of the wave must call this.
+constexpr uint64_t CANON_RANK_MAX = 512;
+
+// (digest, tiebreak) order of two sort records; SET records tie-break on nothing (equal digests
+// are equal records), MAP records carry the wire index in word 8 while they are sorted
+template <bool MAP>
+__device__ __forceinline__ bool canon_less(const u32 a[9], const u32 b[9]) {
+  const int c = dig_cmp(a, b);
+  return c < 0 || (MAP && c == 0 && a[8] < b[8]);
+}
+
+// Ascending sort of cnt records of W words in dst: the bitonic network whose comparators all put
+// the minimum at the lower index (the first merge step of each block compares i with its mirror
+// i ^ (k - 1)), so records past cnt act as +infinity and every comparator touching one is a no-op.
+template <int W, bool MAP>
+__device__ void canon_bitonic(u32* dst, uint64_t cnt, u32 lane) {
+  uint64_t N = 1;
+  while (N < cnt) N <<= 1;
+  for (uint64_t k = 2; k <= N; k <<= 1) {
+    for (uint64_t j = k >> 1; j >= 1; j >>= 1) {
+      const bool flip = j == (k >> 1);
+      for (uint64_t p = lane; p < N / 2; p += 64) {
+        const uint64_t i = (p / j) * 2 * j + (p % j);
+        const uint64_t l = flip ? (i ^ (k - 1)) : (i + j);
+        if (l >= cnt) continue;
+        u32 a[9], b[9];
+        _Pragma("unroll") for (int w = 0; w < 9; ++w) {
+          a[w] = w < W ? dst[W * i + w] : 0u;
+          b[w] = w < W ? dst[W * l + w] : 0u;
+        }
+        if (canon_less<MAP>(b, a)) {
+          _Pragma("unroll") for (int w = 0; w < W; ++w) {
+            dst[W * i + w] = b[w];
+            dst[W * l + w] = a[w];
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 template <int WORDS, bool MAP>
 __device__ uint64_t canon_entries(const uint8_t* base, uint64_t src, uint64_t cnt, u32* dst, u32 lane) {
   constexpr uint64_t REC = 4 * WORDS;
@@ -345,20 +389,37 @@ __device__ uint64_t canon_entries(const uint8_t* base, uint64_t src, uint64_t cn
     __syncthreads();
     return cnt;
   }
-  for (uint64_t e = lane; e < cnt; e += 64) {
-    u32 x[WORDS];
-    ld_words<WORDS>(base, src + REC * e, x);
-    uint64_t pos = 0;
+  if (cnt <= CANON_RANK_MAX) {
+    for (uint64_t e = lane; e < cnt; e += 64) {
+      u32 x[WORDS];
+      ld_words<WORDS>(base, src + REC * e, x);
+      uint64_t pos = 0;
 #pragma unroll 1
-    for (uint64_t j = 0; j < cnt; ++j) {
-      u32 y[8];
-      ld_words<8>(base, src + REC * j, y);
-      const int c = dig_cmp(y, x);
-      pos += (c < 0 || (c == 0 && j < e)) ? 1u : 0u;
+      for (uint64_t j = 0; j < cnt; ++j) {
+        u32 y[8];
+        ld_words<8>(base, src + REC * j, y);
+        const int c = dig_cmp(y, x);
+        pos += (c < 0 || (c == 0 && j < e)) ? 1u : 0u;
+      }
+      _Pragma("unroll") for (int k = 0; k < WORDS; ++k) dst[WORDS * pos + k] = x[k];
     }
-    _Pragma("unroll") for (int k = 0; k < WORDS; ++k) dst[WORDS * pos + k] = x[k];
+    __syncthreads();
+  } else {
+    // records (digest, wire index) for MAP, (digest) for SET, sorted in place; MAP's worker ids are
+    // fetched back from the wire by index once the order is known
+    for (uint64_t e = lane; e < cnt; e += 64) {
+      u32 x[8];
+      ld_words<8>(base, src + REC * e, x);
+      _Pragma("unroll") for (int k = 0; k < 8; ++k) dst[WORDS * e + k] = x[k];
+      if constexpr (MAP) dst[WORDS * e + 8] = (u32)e;
+    }
+    __syncthreads();
+    canon_bitonic<WORDS, MAP>(dst, cnt, lane);
+    if constexpr (MAP) {
+      for (uint64_t e = lane; e < cnt; e += 64) dst[WORDS * e + 8] = ld_u32(base, src + REC * dst[WORDS * e + 8] + 32);
+      __syncthreads();
+    }
   }
-  __syncthreads();
   // Compaction: step s reads entries [64 s, 64 s + 64] and writes only below 64 s + 64, so no
   // step reads what an earlier step wrote; within a step every store depends on every load.
   uint64_t kept = 0;

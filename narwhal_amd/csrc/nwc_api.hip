@@ -17,6 +17,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <random>
 #include <string>
 #include <thread>
 #include <unordered_set>
@@ -118,6 +119,11 @@ struct DevCtx {
   nwc::ge_p3* kb_bases = nullptr;           // key comb window bases (scratch of build_key_combs)
   size_t kb_cap = 0;
   int comb_blocks_per_cu = 1;
+  uint8_t* straus_scratch = nullptr;   // k_verify_straus per-lane tables (nwc_dev_verify_batch_straus)
+  size_t straus_cap = 0;
+  uint64_t* straus_cert = nullptr;     // its certificate verdict words
+  size_t straus_cert_cap = 0;
+  uint32_t* straus_max = nullptr;      // largest certificate of the launch
   uint32_t* uc_list = nullptr;     // k_verify_comb: equations whose key is not cached
   uint32_t* uc_count = nullptr;
   // k_verify per-lane table slots; reused by every launch, so launches that use it are
@@ -165,6 +171,8 @@ struct DevCtx {
   nwc::ge_niels_pad* ak_comb = nullptr;
   int32_t* ak_slots = nullptr;
   uint32_t ak_n = 0, ak_cap = 0, ak_slot_cap = 0;
+  uint32_t ak_evict = 0;                  // next FIFO position once the cache is full
+  uint64_t ak_builds = 0, ak_hits = 0;    // insert batches built / calls served from the auto cache
   KeyIndex ak_host;                       // host copy of the auto cache's lookup table
   std::unordered_set<std::string> ak_seen;   // keys seen once (32-byte strings), bounded
   // copy sources of the last auto-cache build, alive until the stream has passed it
@@ -242,6 +250,10 @@ struct Carve {
   template <class T> T* take(size_t bytes) { T* p = reinterpret_cast<T*>(base + off); off += align256(bytes); return p; }
 };
 
+uint32_t auto_keys_cap();
+int auto_grow(DevCtx& d, uint32_t ncap);
+bool comb16_enabled();
+
 int init_device(DevCtx& d) {
   HIP_TRY(hipSetDevice(d.hip_id));
   hipDeviceProp_t prop;
@@ -266,13 +278,16 @@ int init_device(DevCtx& d) {
   hipLaunchKernelGGL(nwc::k_build_comb<nwc::BaseComb>, dim3((unsigned)((nwc::BaseComb::per + 255) / 256)), dim3(256), 0, d.stream,
                      (const nwc::u32*)nullptr, 1u, d.comb_base);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMalloc(&d.comb16, nwc::COMB16_TOTAL * sizeof(nwc::ge_niels_pad)));
-  HIP_TRY(hipMalloc(&d.comb16_bases, nwc::COMB16_WINDOWS * sizeof(nwc::ge_p3)));
-  hipLaunchKernelGGL(nwc::k_bcomb_bases, dim3(1), dim3(64), 0, d.stream, d.comb16_bases);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(nwc::k_build_comb16, dim3((unsigned)((nwc::COMB16_TOTAL + 255) / 256)), dim3(256), 0, d.stream,
-                     d.comb16, (const nwc::ge_p3*)d.comb16_bases);
-  HIP_TRY(hipGetLastError());
+  if (comb16_enabled()) {
+    // radix-2^22 basepoint comb (3.2 GB): the committee comb kernel and the cold kernel's s B
+    HIP_TRY(hipMalloc(&d.comb16, nwc::COMB16_TOTAL * sizeof(nwc::ge_niels_pad)));
+    HIP_TRY(hipMalloc(&d.comb16_bases, nwc::COMB16_WINDOWS * sizeof(nwc::ge_p3)));
+    hipLaunchKernelGGL(nwc::k_bcomb_bases, dim3(1), dim3(64), 0, d.stream, d.comb16_bases);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(nwc::k_build_comb16, dim3((unsigned)((nwc::COMB16_TOTAL + 255) / 256)), dim3(256), 0, d.stream,
+                       d.comb16, (const nwc::ge_p3*)d.comb16_bases);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipMalloc(&d.base_table, 2 * 129 * sizeof(nwc::ge_niels)));
   HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
   hipLaunchKernelGGL(nwc::k_build_base_table, dim3(5), dim3(64), 0, d.stream, d.base_table);
@@ -288,6 +303,17 @@ int init_device(DevCtx& d) {
   HIP_TRY(hipMalloc(&d.km_keys, 32 * (size_t)NWC_MEMO_SLOTS));
   HIP_TRY(hipMalloc(&d.km_flag, 4 * (size_t)NWC_MEMO_SLOTS));
   HIP_TRY(hipMemsetAsync(d.km_flag, 0xFF, 4 * (size_t)NWC_MEMO_SLOTS, d.stream));
+  // auto key cache: the first AUTO_INIT_KEYS keys' arrays (~330 MB), their slot table and the key
+  // comb builder's scratch are allocated here, so the call that first fills the cache only
+  // queues its build (growth beyond this is stream-ordered, auto_grow)
+  if (const uint32_t acap = auto_keys_cap()) {
+    if (int rc = auto_grow(d, std::min<uint32_t>(acap, 16u))) return rc;
+    d.ak_slot_cap = 64;
+    while (d.ak_slot_cap < 8 * std::min<uint32_t>(acap, 16u)) d.ak_slot_cap <<= 1;
+    HIP_TRY(hipMalloc(&d.ak_slots, 4 * (size_t)d.ak_slot_cap));
+    d.kb_cap = 64 * (size_t)nwc::KeyComb::windows;
+    HIP_TRY(hipMalloc(&d.kb_bases, d.kb_cap * sizeof(nwc::ge_p3)));
+  }
   HIP_TRY(hipStreamSynchronize(d.stream));
   return 0;
 }
@@ -303,15 +329,16 @@ int require_init() {
 }
 
 // Per-key combs of m keys (KeyComb) into out: window bases first, then one lane per entry.  The
-// caller synchronizes the stream before kb_bases is reused.
+// bases are re-allocated stream-ordered when a larger build needs more.
 int build_key_combs(DevCtx& d, const nwc::u32* keys, uint32_t m, nwc::ge_niels_pad* out) {
   if (m == 0) return 0;
   const size_t need = (size_t)m * nwc::KeyComb::windows;
   if (need > d.kb_cap) {
-    if (d.kb_bases) HIP_TRY(hipFree(d.kb_bases));
+    // stream-ordered: the old bases are freed behind the launches that read them
+    if (d.kb_bases) HIP_TRY(hipFreeAsync(d.kb_bases, d.stream));
     d.kb_bases = nullptr;
     d.kb_cap = 0;
-    HIP_TRY(hipMalloc(&d.kb_bases, need * sizeof(nwc::ge_p3)));
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d.kb_bases), need * sizeof(nwc::ge_p3), d.stream));
     d.kb_cap = need;
   }
   hipLaunchKernelGGL(nwc::k_comb_key_bases<nwc::KeyComb>, dim3((m + 63) / 64), dim3(64), 0, d.stream, keys, m, d.kb_bases);
@@ -332,19 +359,73 @@ uint32_t auto_keys_cap() {
   }();
   return cap;
 }
+// NWC_COMB16=0: no radix-2^22 basepoint comb at nwc_init (saves 3.2 GB of HBM per device);
+// committee batches then take the cached ladder (k_verify<true, true>) instead of the comb
+// kernel, and first-sight small calls the one-lane path instead of the cold kernel.
+bool comb16_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NWC_COMB16");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 constexpr size_t AUTO_SEEN_MAX = 4096;   // keys remembered as seen once (cleared when full)
+constexpr uint32_t AUTO_INIT_KEYS = 16;   // auto-cache capacity allocated at nwc_init (doubled on demand)
+
+// Stream-ordered (re)allocation of the auto cache's arrays to ncap keys: the new arrays come from
+// the stream's pool (hipMallocAsync), what is built is copied over, and the old arrays are freed
+// behind every launch already queued -- the host never waits.  Caller holds d.mu.
+int auto_grow(DevCtx& d, uint32_t ncap) {
+  nwc::u32 *keys = nullptr, *flags = nullptr;
+  nwc::ge_niels* tables = nullptr;
+  nwc::ge_niels_pad* comb = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&keys), 32 * (size_t)ncap, d.stream));
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&flags), 4 * (size_t)ncap, d.stream));
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tables), (size_t)ncap * 129 * sizeof(nwc::ge_niels), d.stream));
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&comb), (size_t)ncap * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad),
+                         d.stream));
+  const size_t n0 = d.ak_n;
+  if (n0) {
+    HIP_TRY(hipMemcpyAsync(keys, d.ak_keys, 32 * n0, hipMemcpyDeviceToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(flags, d.ak_flags, 4 * n0, hipMemcpyDeviceToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(tables, d.ak_tables, n0 * 129 * sizeof(nwc::ge_niels), hipMemcpyDeviceToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(comb, d.ak_comb, n0 * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad), hipMemcpyDeviceToDevice,
+                           d.stream));
+  }
+  if (d.ak_keys) HIP_TRY(hipFreeAsync(d.ak_keys, d.stream));
+  if (d.ak_flags) HIP_TRY(hipFreeAsync(d.ak_flags, d.stream));
+  if (d.ak_tables) HIP_TRY(hipFreeAsync(d.ak_tables, d.stream));
+  if (d.ak_comb) HIP_TRY(hipFreeAsync(d.ak_comb, d.stream));
+  d.ak_keys = keys; d.ak_flags = flags; d.ak_tables = tables; d.ak_comb = comb;
+  d.ak_cap = ncap;
+  return 0;
+}
+
+// Empties the auto cache (nwc_set_committee: a new committee makes the remembered keys stale).
+// The arrays are kept for reuse.  Caller holds d.mu and has drained d.stream.
+void auto_reset(DevCtx& d) {
+  d.ak_n = 0;
+  d.ak_evict = 0;
+  d.ak_pending = false;
+  d.ak_host = KeyIndex{};
+  d.ak_seen.clear();
+}
 
 // Keys of a small host call that missed every cache: a key seen before is added to the auto
 // cache (flags, 129-entry table and comb built on d.stream after this call's work; the next call
-// on this device is ordered after the build), a new one is remembered as seen.  The host copy
-// is updated once the build is enqueued; the call does not wait for it (its copy sources stay
-// in d.ak_pend_* until the next build has synchronised).  Caller holds d.mu and has set the device.
+// on this device is ordered after the build), a new one is remembered as seen.  Once the cache
+// holds NWC_AUTO_KEYS keys, new ones replace the oldest (FIFO ring): a launch queued before the
+// replacement has finished with the old entry when the build runs (one stream), and the host
+// index drops the old key at once, so its next call takes the uncached path.  The host copy is
+// updated once the build is enqueued; the call does not wait for it (its copy sources stay in
+// d.ak_pend_* until the next build has synchronised).  Caller holds d.mu and has set the device.
 int auto_insert(DevCtx& d, const uint8_t* pks, uint64_t n) {
   const uint32_t cap = auto_keys_cap();
-  if (cap == 0 || d.ak_n >= cap) return 0;
+  if (cap == 0) return 0;
   std::vector<nwc::u32> add;
   std::unordered_set<std::string> added;
-  for (uint64_t i = 0; i < n && d.ak_n + add.size() / 8 < cap; ++i) {
+  for (uint64_t i = 0; i < n && add.size() / 8 < cap; ++i) {
     const uint8_t* k = pks + 32 * i;
     if (d.ak_host.find(k)) continue;
     std::string ks(reinterpret_cast<const char*>(k), 32);
@@ -364,58 +445,52 @@ int auto_insert(DevCtx& d, const uint8_t* pks, uint64_t n) {
     HIP_TRY(hipStreamSynchronize(d.stream));   // the previous build's copy sources are free again
     d.ak_pending = false;
   }
-  const uint32_t n0 = d.ak_n, n1 = n0 + m;
-  if (n1 > d.ak_cap) {
-    // grow (doubling, at most the configured capacity): copy what is built, free the old arrays
-    // once the stream has drained
-    const uint32_t ncap = std::min(cap, std::max<uint32_t>(16u, 2 * n1));
-    nwc::u32 *keys = nullptr, *flags = nullptr;
-    nwc::ge_niels* tables = nullptr;
-    nwc::ge_niels_pad* comb = nullptr;
-    HIP_TRY(hipMalloc(&keys, 32 * (size_t)ncap));
-    HIP_TRY(hipMalloc(&flags, 4 * (size_t)ncap));
-    HIP_TRY(hipMalloc(&tables, (size_t)ncap * 129 * sizeof(nwc::ge_niels)));
-    HIP_TRY(hipMalloc(&comb, (size_t)ncap * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad)));
-    if (n0) {
-      HIP_TRY(hipMemcpyAsync(keys, d.ak_keys, 32 * (size_t)n0, hipMemcpyDeviceToDevice, d.stream));
-      HIP_TRY(hipMemcpyAsync(flags, d.ak_flags, 4 * (size_t)n0, hipMemcpyDeviceToDevice, d.stream));
-      HIP_TRY(hipMemcpyAsync(tables, d.ak_tables, (size_t)n0 * 129 * sizeof(nwc::ge_niels), hipMemcpyDeviceToDevice, d.stream));
-      HIP_TRY(hipMemcpyAsync(comb, d.ak_comb, (size_t)n0 * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad),
-                             hipMemcpyDeviceToDevice, d.stream));
+  // positions: append while there is room, then the FIFO ring over [0, cap)
+  std::vector<uint32_t> pos(m);
+  uint32_t n1 = d.ak_n;
+  for (uint32_t j = 0; j < m; ++j) {
+    if (n1 < cap) {
+      pos[j] = n1++;
+    } else {
+      pos[j] = d.ak_evict;
+      d.ak_evict = (d.ak_evict + 1) % cap;
     }
-    HIP_TRY(hipStreamSynchronize(d.stream));
-    if (d.ak_keys) HIP_TRY(hipFree(d.ak_keys));
-    if (d.ak_flags) HIP_TRY(hipFree(d.ak_flags));
-    if (d.ak_tables) HIP_TRY(hipFree(d.ak_tables));
-    if (d.ak_comb) HIP_TRY(hipFree(d.ak_comb));
-    d.ak_keys = keys; d.ak_flags = flags; d.ak_tables = tables; d.ak_comb = comb;
-    d.ak_cap = ncap;
   }
+  if (n1 > d.ak_cap)
+    if (int rc = auto_grow(d, std::min(cap, std::max<uint32_t>(AUTO_INIT_KEYS, 2 * n1)))) return rc;
   KeyIndex next = d.ak_host;
-  next.keys.insert(next.keys.end(), add.begin(), add.end());
+  next.keys.resize(8 * (size_t)n1);
+  for (uint32_t j = 0; j < m; ++j) std::memcpy(&next.keys[8 * (size_t)pos[j]], &add[8 * (size_t)j], 32);
   std::vector<int32_t> table;
   const uint32_t slots = build_slots(next.keys, n1, table);
   if (slots > d.ak_slot_cap) {
-    HIP_TRY(hipStreamSynchronize(d.stream));   // no launch still reads the old slot table
-    if (d.ak_slots) HIP_TRY(hipFree(d.ak_slots));
+    if (d.ak_slots) HIP_TRY(hipFreeAsync(d.ak_slots, d.stream));   // after every launch that reads it
     d.ak_slots = nullptr;
-    HIP_TRY(hipMalloc(&d.ak_slots, 4 * (size_t)slots));
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d.ak_slots), 4 * (size_t)slots, d.stream));
     d.ak_slot_cap = slots;
   }
   d.ak_pend_keys = std::move(add);
   d.ak_pend_slots = table;
-  HIP_TRY(hipMemcpyAsync(d.ak_keys + 8 * (size_t)n0, d.ak_pend_keys.data(), 32 * (size_t)m, hipMemcpyHostToDevice,
-                         d.stream));
-  hipLaunchKernelGGL(nwc::k_build_key_tables, dim3((unsigned)((m * 129 + 255) / 256)), dim3(256), 0, d.stream,
-                     d.ak_keys + 8 * (size_t)n0, m, d.ak_tables + (size_t)n0 * 129, d.ak_flags + n0);
-  HIP_TRY(hipGetLastError());
-  if (int rc = build_key_combs(d, d.ak_keys + 8 * (size_t)n0, m, d.ak_comb + (size_t)n0 * nwc::COMB_PER_KEY)) return rc;
+  // contiguous runs of positions (at most two: the appended tail and the ring's start)
+  for (uint32_t j0 = 0; j0 < m;) {
+    uint32_t j1 = j0 + 1;
+    while (j1 < m && pos[j1] == pos[j1 - 1] + 1) ++j1;
+    const uint32_t p0 = pos[j0], r = j1 - j0;
+    HIP_TRY(hipMemcpyAsync(d.ak_keys + 8 * (size_t)p0, d.ak_pend_keys.data() + 8 * (size_t)j0, 32 * (size_t)r,
+                           hipMemcpyHostToDevice, d.stream));
+    hipLaunchKernelGGL(nwc::k_build_key_tables, dim3((unsigned)((r * 129 + 255) / 256)), dim3(256), 0, d.stream,
+                       d.ak_keys + 8 * (size_t)p0, r, d.ak_tables + (size_t)p0 * 129, d.ak_flags + p0);
+    HIP_TRY(hipGetLastError());
+    if (int rc = build_key_combs(d, d.ak_keys + 8 * (size_t)p0, r, d.ak_comb + (size_t)p0 * nwc::COMB_PER_KEY)) return rc;
+    j0 = j1;
+  }
   HIP_TRY(hipMemcpyAsync(d.ak_slots, d.ak_pend_slots.data(), 4 * (size_t)slots, hipMemcpyHostToDevice, d.stream));
   d.ak_pending = true;
   next.slots = std::move(table);
   next.mask = slots - 1;
   d.ak_host = std::move(next);
   d.ak_n = n1;
+  ++d.ak_builds;
   return 0;
 }
 
@@ -514,7 +589,7 @@ int launch_torsion(DevCtx& d, const uint8_t* pks, uint64_t* out_words, uint64_t 
 bool cold_path() {
   static const bool on = [] {
     const char* e = std::getenv("NWC_COLD");
-    return !(e && std::strcmp(e, "0") == 0);
+    return !(e && std::strcmp(e, "0") == 0) && comb16_enabled();   // its s B is a comb16 sum
   }();
   return on;
 }
@@ -543,6 +618,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const VPath path = verify_path();
   if ((flags & LV_AUTO) && (flags & LV_ALL_CACHED) && path == VPath::Default && n <= NWC_WIDE_MAX && d.ak_n) {
     // latency path over the auto key cache (same kernel, the auto cache as its committee)
+    ++d.ak_hits;
     const nwc::Committee cm{d.ak_keys, d.ak_flags, d.ak_tables, d.ak_comb, d.ak_slots, d.ak_host.mask, d.ak_n};
     const nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24,
                             d.scratch, d.fb_list, d.fb_count, 0u, cm};
@@ -566,7 +642,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     HIP_TRY(hipGetLastError());
     return 0;
   }
-  const bool comb = path == VPath::Default && d.cm_n && d.cm_comb;
+  // (the throughput comb kernel needs the basepoint comb16; the latency kernel does not)
+  const bool comb = path == VPath::Default && d.cm_n && d.cm_comb && (n <= NWC_WIDE_MAX || d.comb16);
   if (comb && n <= NWC_WIDE_MAX && (flags & LV_ALL_CACHED)) {
     // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none).
     // The host checked every key against its view of the cache (set under g_cm_mu, like the
@@ -986,6 +1063,9 @@ void nwc_shutdown(void) {
     if (d->comb16) (void)hipFree(d->comb16);
     if (d->comb16_bases) (void)hipFree(d->comb16_bases);
     if (d->kb_bases) (void)hipFree(d->kb_bases);
+    if (d->straus_scratch) (void)hipFree(d->straus_scratch);
+    if (d->straus_cert) (void)hipFree(d->straus_cert);
+    if (d->straus_max) (void)hipFree(d->straus_max);
     if (d->pinned) (void)hipHostFree(d->pinned);
     if (d->cc_stakes) (void)hipFree(d->cc_stakes);
     if (d->cc_worker_off) (void)hipFree(d->cc_worker_off);
@@ -1136,6 +1216,7 @@ static int set_committee_locked(const uint8_t* pks, size_t n) {
     HIP_TRY(hipSetDevice(d.hip_id));
     HIP_TRY(hipEventSynchronize(d.scratch_free));   // no verify launch still reads the old cache
     HIP_TRY(hipStreamSynchronize(d.stream));
+    auto_reset(d);   // keys remembered under the old committee are stale
     if (d.cm_keys) HIP_TRY(hipFree(d.cm_keys));
     if (d.cm_flags) HIP_TRY(hipFree(d.cm_flags));
     if (d.cm_tables) HIP_TRY(hipFree(d.cm_tables));
@@ -1185,6 +1266,16 @@ int nwc_cache_stats(uint32_t* committee_keys, uint32_t* auto_keys) {
   std::lock_guard<std::mutex> lk(d.mu);
   if (committee_keys) *committee_keys = d.cm_n;
   if (auto_keys) *auto_keys = d.ak_n;
+  return 0;
+}
+
+int nwc_auto_cache_info(uint32_t* capacity, uint64_t* builds, uint64_t* hits) {
+  if (int rc = require_init()) return rc;
+  DevCtx& d = *ctx(t_dev < (int)g_devs.size() ? t_dev : 0);
+  std::lock_guard<std::mutex> lk(d.mu);
+  if (capacity) *capacity = auto_keys_cap();
+  if (builds) *builds = d.ak_builds;
+  if (hits) *hits = d.ak_hits;
   return 0;
 }
 
@@ -1272,6 +1363,84 @@ int nwc_dev_cert_reduce(const void* d_leaf_words, const void* d_offsets, uint64_
   DEV_PROLOGUE
   return launch_cert_reduce((const uint64_t*)d_leaf_words, (const uint32_t*)d_offsets, m, nvotes,
                             (uint64_t*)d_cert_words, (uint64_t*)d_bad_words, s);
+}
+
+int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, const void* d_msg_index, uint64_t m,
+                                uint64_t nvotes, const void* d_pks, const void* d_sigs, void* d_leaf_words,
+                                void* stream) {
+  DEV_PROLOGUE
+  if (m == 0 || nvotes == 0) return 0;
+  if (!d_digests || !d_offsets || !d_msg_index || !d_pks || !d_sigs || !d_leaf_words)
+    return set_err(NWC_ERR_ARG, "null buffer");
+  const auto* dig = static_cast<const uint8_t*>(d_digests);
+  const auto* voffs = static_cast<const uint32_t*>(d_offsets);
+  const auto* mi = static_cast<const uint32_t*>(d_msg_index);
+  const auto* pks = static_cast<const uint8_t*>(d_pks);
+  const auto* sigs = static_cast<const uint8_t*>(d_sigs);
+  auto* leaf = static_cast<uint64_t*>(d_leaf_words);
+  // the largest certificate decides how many lanes share one (each lane holds <= 24 votes)
+  if (!d.straus_max) HIP_TRY(hipMalloc(&d.straus_max, sizeof(uint32_t)));
+  HIP_TRY(hipMemsetAsync(d.straus_max, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(nwc::k_cert_maxlen, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, voffs, m, d.straus_max);
+  HIP_TRY(hipGetLastError());
+  uint32_t maxv = 0;
+  HIP_TRY(hipMemcpyAsync(&maxv, d.straus_max, sizeof maxv, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  uint32_t L = 1;
+  while (L < 64 && (maxv + L - 1) / L > (uint32_t)nwc::STRAUS_MAX_PER_LANE) L <<= 1;
+  if (!d.comb16 || (maxv + L - 1) / L > (uint32_t)nwc::STRAUS_MAX_PER_LANE)
+    // no basepoint comb (NWC_COMB16=0) or certificates of > 1,536 votes: the exact leaves
+    return launch_verify(d, dig, mi, 0, pks, sigs, nvotes, 0, leaf, s);
+  const uint64_t resident = (uint64_t)d.cus * 2 * 256;
+  const uint64_t lanes = std::min<uint64_t>((m * L + 255) / 256 * 256, resident);
+  const uint64_t stride = (uint64_t)((maxv + L - 1) / L) * nwc::STRAUS_VOTE_BYTES;
+  if (lanes * stride > d.straus_cap || (m + 63) / 64 > d.straus_cert_cap) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (lanes * stride > d.straus_cap) {
+      if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
+      d.straus_scratch = nullptr;
+      d.straus_cap = 0;
+      HIP_TRY(hipMalloc(&d.straus_scratch, lanes * stride));
+      d.straus_cap = lanes * stride;
+    }
+    if ((m + 63) / 64 > d.straus_cert_cap) {
+      if (d.straus_cert) HIP_TRY(hipFree(d.straus_cert));
+      d.straus_cert = nullptr;
+      d.straus_cert_cap = 0;
+      HIP_TRY(hipMalloc(&d.straus_cert, 8 * ((m + 63) / 64)));
+      d.straus_cert_cap = (m + 63) / 64;
+    }
+  }
+  // the failing certificates' leaves: the list-mode leaf kernel's scratch and lists
+  const uint64_t lgrid = (uint64_t)d.cus * d.verify_blocks_per_cu;
+  if (int rc = ensure_scratch(d, (size_t)lgrid * 256 * 2 * nwc::TAB_BYTES_PER_LANE, nvotes)) return rc;
+  HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
+  nwc::StrausArgs sa{};
+  sa.digests = dig; sa.voffs = voffs; sa.pks = pks; sa.sigs = sigs; sa.m = m; sa.lanes_per_cert = L;
+  {
+    // 32 bytes from the host's CSPRNG per launch (dalek: merlin transcript + thread_rng)
+    static thread_local std::random_device rd;
+    for (int i = 0; i < 8; ++i) sa.seed[i] = rd();
+  }
+  sa.comb16 = d.comb16; sa.scratch = d.straus_scratch; sa.lane_stride = stride; sa.cert_words = d.straus_cert;
+  HIP_TRY(hipMemsetAsync(d.straus_cert, 0, 8 * ((m + 63) / 64), s));
+  HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(nwc::k_verify_straus, dim3((unsigned)(lanes / 256)), dim3(256), 0, s, sa);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_straus_expand, dim3((unsigned)((nvotes + 255) / 256)), dim3(256), 0, s,
+                     (const uint64_t*)d.straus_cert, mi, nvotes, leaf, d.uc_list, d.uc_count);
+  HIP_TRY(hipGetLastError());
+  const nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
+                          d.fb_count, 0u, nwc::Committee{}};
+  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
+  hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3((unsigned)lgrid), dim3(256), 0, s, a, ca);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(16), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  if (int rc = launch_torsion(d, pks, leaf, nvotes, d.uc_list, d.uc_count, nwc::Committee{}, s)) return rc;
+  HIP_TRY(hipEventRecord(d.scratch_free, s));
+  return 0;
 }
 
 int nwc_dev_sha512_trunc32(const void* d_data, const void* d_offsets, uint64_t n, void* d_out32, void* stream) {
@@ -1519,3 +1688,5 @@ int nwc_dev_sanitize_messages(const void* d_data, const void* d_offsets, uint64_
 }
 
 }  // extern "C"
+
+#include "digester.h"

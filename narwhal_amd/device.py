@@ -48,6 +48,21 @@ def verify(msgs: torch.Tensor, pks: torch.Tensor, sigs: torch.Tensor, strict: bo
     return out
 
 
+def verify_batch_straus(digests: torch.Tensor, offsets: torch.Tensor, msg_index: torch.Tensor, pks: torch.Tensor,
+                        sigs: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dalek's batch equation per certificate (Straus), the exact leaves for the certificates it
+    rejects: returns leaf-style verdict words (bit per vote) for cert_reduce.  Asynchronous."""
+    lib = _lib.load()
+    m = offsets.numel() - 1
+    n = pks.shape[0]
+    assert offsets.dtype == torch.int32 and msg_index.dtype == torch.int32 and msg_index.numel() == n
+    if out is None:
+        out = torch.empty(words_for(n), dtype=torch.int64, device=pks.device)
+    _lib.check(lib.nwc_dev_verify_batch_straus(_ptr(digests), _ptr(offsets), _ptr(msg_index), m, n, _ptr(pks),
+                                               _ptr(sigs), _ptr(out), _stream()))
+    return out
+
+
 def cert_reduce(leaf_words: torch.Tensor, offsets: torch.Tensor, nvotes: int,
                 want_bad: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     lib = _lib.load()

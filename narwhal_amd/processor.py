@@ -1,0 +1,141 @@
+"""The worker's `Processor` (worker/src/processor.rs:20-56) over the GPU batch digester.
+
+The reference task loops `while let Some(batch) = rx_batch.recv().await`, hashes each batch with
+`Sha512::digest(&batch)[..32]` (:38), stores it under its digest (:41) and sends the bincode of
+`WorkerPrimaryMessage::OurBatch(digest, id)` / `OthersBatch(digest, id)` to the primary (:44-53).
+Here the loop hands every batch to a libnwc digester (`nwc_digester_*`, include/nwc.h), whose drain
+thread digests whatever has queued up -- up to `max_group` batches, or what arrived within
+`max_wait_us` of the first -- in one GPU launch; a collector thread then stores each batch and
+sends its message, in arrival order, exactly as the reference does per batch.
+
+There is no CPU path inside: one 500-KB batch alone costs ~30 ms on the GPU (a sequential SHA-512
+chain on one lane) against ~0.36 ms on one host core, so this Processor is for workers that can
+hand batches over in groups (INTEGRATION.md §4 has the measured crossover); a worker sealing one
+batch at a time on a latency-critical path keeps `Sha512::digest`.
+
+Channels are `queue.Queue`s (tokio mpsc's role); `None` on rx_batch closes it (the reference's
+`recv()` returning `None`).  `store` is anything with `write(key: bytes, value: bytes)`.
+"""
+from __future__ import annotations
+
+import ctypes
+import queue
+import struct
+import threading
+from typing import Dict, List, Optional, Tuple
+
+from narwhal_amd import _lib
+
+OUR_BATCH, OTHERS_BATCH = 0, 1   # WorkerPrimaryMessage variants (primary/src/primary.rs)
+
+
+def worker_primary_message(digest: bytes, worker_id: int, own_digest: bool) -> bytes:
+    """bincode::serialize(&WorkerPrimaryMessage::{Our,Others}Batch(digest, id)): u32 variant,
+    the 32 digest bytes, the u32 WorkerId (processor.rs:44-50)."""
+    return struct.pack("<I", OUR_BATCH if own_digest else OTHERS_BATCH) + digest + struct.pack("<I", worker_id)
+
+
+class Digester:
+    """ctypes handle of one `nwc_digester` (its drain thread runs inside libnwc).  Keeps every
+    submitted batch alive until its digest has been polled (the C side borrows it)."""
+
+    def __init__(self, max_group: int = 1024, max_wait_us: int = 1000):
+        self.lib = _lib.load()
+        h = self.lib.nwc_digester_create(max_group, max_wait_us)
+        if not h:
+            raise _lib.DeviceError(self.lib.nwc_last_error().decode())
+        self.h = ctypes.c_void_p(h)
+        self._held: Dict[int, object] = {}
+        self._next = 0
+        self._lock = threading.Lock()
+
+    def submit(self, batch, tag: Optional[int] = None) -> int:
+        """Queue one batch (bytes-like); returns its tag (a sequence number unless given)."""
+        buf = _lib.buf(batch)
+        n = batch.nbytes if hasattr(batch, "nbytes") else len(batch)
+        with self._lock:
+            if tag is None:
+                tag = self._next
+            self._next = max(self._next, tag + 1)
+            self._held[tag] = (batch, buf)
+        _lib.check(self.lib.nwc_digester_submit(self.h, buf, n, tag))
+        return tag
+
+    def poll(self, max_n: int = 4096, wait_us: int = 0) -> List[Tuple[int, bytes]]:
+        tags = (ctypes.c_uint64 * max_n)()
+        digs = ctypes.create_string_buffer(32 * max_n)
+        n = ctypes.c_size_t(0)
+        rc = self.lib.nwc_digester_poll(self.h, max_n, wait_us, tags, digs, ctypes.byref(n))
+        out = [(int(tags[i]), digs.raw[32 * i:32 * i + 32]) for i in range(n.value)]
+        with self._lock:
+            for t, _ in out:
+                self._held.pop(t, None)
+        _lib.check(rc)
+        return out
+
+    def stats(self) -> Tuple[int, int, int]:
+        g, b, by = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(self.lib.nwc_digester_stats(self.h, ctypes.byref(g), ctypes.byref(b), ctypes.byref(by)))
+        return g.value, b.value, by.value
+
+    def close(self) -> None:
+        if self.h:
+            rc = self.lib.nwc_digester_destroy(self.h)
+            self.h = None
+            _lib.check(rc)
+
+
+class Processor:
+    """`Processor::spawn(id, store, rx_batch, tx_digest, own_digest)` (processor.rs:22-34)."""
+
+    def __init__(self, worker_id: int, store, rx_batch: "queue.Queue", tx_digest: "queue.Queue", own_digest: bool,
+                 max_group: int = 1024, max_wait_us: int = 1000):
+        self.id, self.store, self.rx, self.tx, self.own = worker_id, store, rx_batch, tx_digest, own_digest
+        self.dg = Digester(max_group, max_wait_us)
+        self._pending: Dict[int, bytes] = {}
+        self._submitted = 0
+        self._done = 0
+        self._closed = threading.Event()
+        self._error: Optional[BaseException] = None
+        self._feeder = threading.Thread(target=self._feed, daemon=True)
+        self._collector = threading.Thread(target=self._collect, daemon=True)
+        self._feeder.start()
+        self._collector.start()
+
+    @classmethod
+    def spawn(cls, worker_id: int, store, rx_batch, tx_digest, own_digest: bool, **kw) -> "Processor":
+        return cls(worker_id, store, rx_batch, tx_digest, own_digest, **kw)
+
+    def _feed(self):
+        try:
+            while True:
+                batch = self.rx.get()
+                if batch is None:   # channel closed
+                    break
+                tag = self._submitted
+                self._pending[tag] = batch
+                self._submitted += 1
+                self.dg.submit(batch, tag)
+        except BaseException as e:  # noqa: BLE001 (reported by join())
+            self._error = e
+        finally:
+            self._closed.set()
+
+    def _collect(self):
+        try:
+            while not (self._closed.is_set() and self._done == self._submitted):
+                for tag, digest in self.dg.poll(4096, 2000):
+                    batch = self._pending.pop(tag)
+                    self.store.write(digest, batch)                                   # :41
+                    self.tx.put(worker_primary_message(digest, self.id, self.own))    # :44-53
+                    self._done += 1
+        except BaseException as e:  # noqa: BLE001
+            self._error = e
+
+    def join(self, timeout: Optional[float] = None) -> None:
+        """Wait until the closed channel's last batch has been stored and sent; frees the digester."""
+        self._feeder.join(timeout)
+        self._collector.join(timeout)
+        self.dg.close()
+        if self._error:
+            raise self._error

@@ -13,8 +13,9 @@ import numpy as np
 
 
 def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
-    """Contiguous [lo, hi) of n units for `rank`; shards differ in size by at most one unit and
-    every shard except possibly the last starts on a multiple of 64 (whole verdict words)."""
+    """Contiguous [lo, hi) of n units for `rank`, cut on whole 64-unit verdict words: every shard
+    starts on a multiple of 64, each holds ceil(ceil(n / 64) / world) words except the tail, so
+    shards can differ by up to 64 * world - 1 units (the last ones may be short or empty)."""
     words = (n + 63) // 64
     per = (words + world - 1) // world
     lo = min(n, rank * per * 64)

@@ -3,6 +3,10 @@
 #![allow(dead_code)]
 use std::os::raw::{c_char, c_int, c_void};
 
+/// Opaque handle of a batch digester (nwc_digester_create).
+#[allow(non_camel_case_types)]
+pub enum nwc_digester {}
+
 #[link(name = "nwc")]
 extern "C" {
     pub fn nwc_init(device_mask: u32) -> c_int;
@@ -19,6 +23,7 @@ extern "C" {
                                  cert_ok_bitmap: *mut u8, bad_vote_bitmap: *mut u8) -> c_int;
     pub fn nwc_set_committee(pks: *const u8, n: usize) -> c_int;
     pub fn nwc_cache_stats(committee_keys: *mut u32, auto_keys: *mut u32) -> c_int;
+    pub fn nwc_auto_cache_info(capacity: *mut u32, builds: *mut u64, hits: *mut u64) -> c_int;
 
     pub fn nwc_set_committee_config(pks: *const u8, stakes: *const u64, n: usize, worker_offsets: *const u32,
                                     worker_ids: *const u32) -> c_int;
@@ -30,12 +35,21 @@ extern "C" {
 
     pub fn nwc_digest32(data: *const u8, len: usize, out32: *mut u8) -> c_int;
     pub fn nwc_sha512_trunc32_many(data: *const u8, offsets: *const u64, n: usize, out32: *mut u8) -> c_int;
+    pub fn nwc_digester_create(max_group: u32, max_wait_us: u32) -> *mut nwc_digester;
+    pub fn nwc_digester_submit(q: *mut nwc_digester, batch: *const u8, len: usize, tag: u64) -> c_int;
+    pub fn nwc_digester_poll(q: *mut nwc_digester, max: usize, wait_us: u32, tags: *mut u64, digests32: *mut u8,
+                             n_done: *mut usize) -> c_int;
+    pub fn nwc_digester_stats(q: *mut nwc_digester, groups: *mut u64, batches: *mut u64, bytes: *mut u64) -> c_int;
+    pub fn nwc_digester_destroy(q: *mut nwc_digester) -> c_int;
 
     pub fn nwc_dev_verify(d_msgs: *const c_void, d_msg_index: *const c_void, msg_stride: u64, d_pks: *const c_void,
                           d_sigs: *const c_void, n: u64, strict: c_int, d_verdict_words: *mut c_void,
                           stream: *mut c_void) -> c_int;
     pub fn nwc_dev_cert_reduce(d_leaf_words: *const c_void, d_offsets: *const c_void, m: u64, nvotes: u64,
                                d_cert_words: *mut c_void, d_bad_words: *mut c_void, stream: *mut c_void) -> c_int;
+    pub fn nwc_dev_verify_batch_straus(d_digests: *const c_void, d_offsets: *const c_void, d_msg_index: *const c_void,
+                                       m: u64, nvotes: u64, d_pks: *const c_void, d_sigs: *const c_void,
+                                       d_leaf_words: *mut c_void, stream: *mut c_void) -> c_int;
     pub fn nwc_dev_sha512_trunc32(d_data: *const c_void, d_offsets: *const c_void, n: u64, d_out32: *mut c_void,
                                   stream: *mut c_void) -> c_int;
     pub fn nwc_dev_sha512_trunc32_ranges(d_data: *const c_void, d_starts: *const c_void, d_ends: *const c_void, n: u64,

@@ -11,17 +11,29 @@
  *                                       -> "C <rc> <cert bitmap> <bad bitmap>" (nwc_verify_batch_many)
  *   X <threads> <rounds>                -> "X <mismatches>": every B request so far re-run from
  *                                          that many concurrent host threads, results compared
+ *   K <n> <pk32> x n                    -> "K <rc>"                 (nwc_set_committee; n = 0 clears)
+ *   L <calls> <warm> <msg32> <n> <pk32 sig64> x n
+ *                                       -> "L <rc> <first> <second> <p50> <p90> <p99> <p99.9> <max> <mean>"
+ *                                          per-call latency (us) of nwc_verify_batch timed in C;
+ *                                          percentiles over calls warm..calls-1
  *   Z                                   -> a heap read one byte out of bounds (sanitizer self-check)
  * Built by __graft_entry__.build() into tests/cpp/build/abi_host (and, host code under
  * AddressSanitizer + UBSan against a sanitized libnwc, abi_host_asan); run by
  * tests/test_gpu_abi_host.py.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "nwc.h"
+
+static int cmp_double(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return (x > y) - (x < y);
+}
 
 /* B requests kept for the X (concurrency) command */
 typedef struct {
@@ -191,6 +203,59 @@ int main(void) {
         mism += (long)v;
       }
       printf("X %ld\n", mism);
+    } else if (tok[0] == 'K') {
+      /* K n pk... : nwc_set_committee (n = 0 clears it) */
+      const char* cnt = strtok(NULL, " \n");
+      if (!cnt) return 3;
+      const size_t n = (size_t)strtoul(cnt, NULL, 10);
+      unsigned char* pks = malloc(32 * n + 1);
+      for (size_t i = 0; i < n; ++i) {
+        const char* p = strtok(NULL, " \n");
+        if (!p || unhex(p, pks + 32 * i, 32)) return 3;
+      }
+      printf("K %d\n", nwc_set_committee(n ? pks : NULL, n));
+      free(pks);
+    } else if (tok[0] == 'L') {
+      /* L calls warm msg n pk sig ... : per-call latency of nwc_verify_batch on one batch, timed
+       * here in C (no interpreter in the loop); prints the first two calls and percentiles of
+       * calls warm.. in microseconds */
+      const char* c1 = strtok(NULL, " \n");
+      const char* c2 = strtok(NULL, " \n");
+      const char* a = strtok(NULL, " \n");
+      const char* cnt = strtok(NULL, " \n");
+      unsigned char m[32];
+      if (!c1 || !c2 || !a || !cnt || unhex(a, m, 32)) return 3;
+      const long calls = atol(c1), warm = atol(c2);
+      const size_t n = (size_t)strtoul(cnt, NULL, 10);
+      unsigned char* pks = malloc(32 * n + 1);
+      unsigned char* sigs = malloc(64 * n + 1);
+      for (size_t i = 0; i < n; ++i) {
+        const char* p = strtok(NULL, " \n");
+        const char* s = strtok(NULL, " \n");
+        if (!p || !s || unhex(p, pks + 32 * i, 32) || unhex(s, sigs + 64 * i, 64)) return 3;
+      }
+      double* us = malloc(sizeof(double) * (size_t)(calls + 1));
+      int rc0 = -100;
+      for (long k = 0; k < calls; ++k) {
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        rc = nwc_verify_batch(m, pks, sigs, n, NULL);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if (k == 0) rc0 = rc;
+        if (rc != rc0) return 4;
+        us[k] = (t1.tv_sec - t0.tv_sec) * 1e6 + (t1.tv_nsec - t0.tv_nsec) * 1e-3;
+      }
+      const double first = us[0], second = calls > 1 ? us[1] : 0;
+      const long cnt2 = calls - warm;
+      double* w = us + warm;
+      qsort(w, (size_t)cnt2, sizeof(double), cmp_double);
+      double sum = 0;
+      for (long k = 0; k < cnt2; ++k) sum += w[k];
+      printf("L %d %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f\n", rc0, first, second, w[cnt2 / 2], w[(long)(cnt2 * 0.9)],
+             w[(long)(cnt2 * 0.99)], w[(long)(cnt2 * 0.999)], w[cnt2 - 1], sum / cnt2);
+      free(us);
+      free(pks);
+      free(sigs);
     } else if (tok[0] == 'Z') {
       /* sanitizer self-check (tests only): one byte read past a heap block must be reported */
       volatile unsigned char* z = malloc(16);

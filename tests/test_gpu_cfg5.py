@@ -3,7 +3,7 @@ cases spread over the golden edge classes (small-order / non-canonical A and R, 
 verified with verify_strict, sharded over ranks, verdict words all-gathered.
 
 * full size on one GPU, in process, through bench.bench_cfg5 (the bench's own leg);
-* the sharded form over 2 and 4 ranks: bench.py under torch.distributed.run with the gloo
+* the sharded form over 2, 4 and 8 ranks (config 5's full width): bench.py under torch.distributed.run with the gloo
   backend, every rank on this box's one GPU (the driver's 8-GPU node runs the same code with RCCL,
   one GPU per rank).  Each rank generates its contiguous shard, verifies it, and the verdict words
   are all-gathered and compared with each rank's own; expected verdicts come from the golden
@@ -30,7 +30,7 @@ def test_cfg5_full_size_one_gpu():
     assert out["per_gpu"] == 64 << 20 and out["edge_slots_per_gpu"] > 600000
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_cfg5_sharded_gloo(world):
     port = 29500 + (os.getpid() * 7 + world) % 2000
     env = dict(os.environ, NWC_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
@@ -39,7 +39,7 @@ def test_cfg5_sharded_gloo(world):
            "--gpus", str(world), "--steps", "1", "--warmup", "1", "--triples", "65536", "--digest-batches", "0",
            "--cpu-budget", "0", "--cfg3-certs", "0", "--cfg1-calls", "0", "--wire-certs", "0",
            "--cfg5-total", str(3 * (1 << 20) + 4096 * world)]
-    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240 + 40 * world)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == world and line["config"]["verdicts_ok"]

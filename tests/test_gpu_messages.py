@@ -232,3 +232,55 @@ def test_mirror_objects(lib):
         assert e.value.name == "InvalidHeaderId"
     finally:
         lib.nwc_set_committee(None, 0)
+
+
+def test_large_unsorted_headers(lib, oracle):
+    """Byzantine headers whose payload map / parent set arrive unsorted, reversed and with duplicates,
+    from small to a near-maximum frame (200k parents = 6.4 MB of the LengthDelimitedCodec's 8 MiB):
+    codes and digests against the restatement, and the big one bounded in time (the bitonic path of
+    messages.h canon_entries; the rank method needed cnt^2 loads)."""
+    import time
+    import messages_ref as mr
+    rng = np.random.default_rng(77)
+    seeds = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(4)]
+    pks = [oracle.public_key(s) for s in seeds]
+    committee = mr.RefCommittee({pk: (1, [0, 1]) for pk in pks})
+    _install(lib, pks, [1] * 4, [[0, 1]] * 4)
+    sig = _CSig(oracle)
+
+    def header(nparents, npayload, ids_on_wire=False):
+        parents = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(nparents)]
+        parents = sorted(parents, reverse=True)
+        parents += [parents[int(i)] for i in rng.integers(0, nparents, max(1, nparents // 10))]
+        parents = [parents[int(i)] for i in rng.permutation(len(parents))] if rng.random() < 0.5 else parents
+        payload = [(bytes(rng.integers(0, 256, 32, dtype=np.uint8)), int(rng.integers(0, 2))) for _ in range(npayload)]
+        payload += [(payload[int(i)][0], int(rng.integers(0, 3))) for i in rng.integers(0, max(1, npayload), npayload // 8)]
+        payload.reverse()
+        if ids_on_wire:   # id over the wire order: InvalidHeaderId
+            b = pks[0] + struct.pack("<Q", 5)
+            b += b"".join(d + struct.pack("<I", w) for d, w in payload) + b"".join(parents)
+            hid = mr.sha512_32(b)
+        else:
+            hid = mr.header_id(pks[0], 5, payload, parents)
+        return mr.msg_header(mr.enc_header(pks[0], 5, payload, parents, hid, oracle.sign(seeds[0], hid),
+                                           wire_order=True))
+
+    try:
+        msgs = [header(n, p, w) for n, p in ((600, 40), (700, 600), (5000, 3000), (20000, 0)) for w in (False, True)]
+        codes, dig, _ = _sanitize(lib, msgs)
+        for i, m in enumerate(msgs):
+            code, kind, d = mr.sanitize(m, committee, sig)
+            assert codes[i] == code, (i, int(codes[i]), mr.NAMES[code])
+            assert dig[i].tobytes() == d, i
+        big = header(200000, 0)
+        assert len(big) < 8 << 20
+        _sanitize(lib, [big])                  # warm-up (allocations)
+        t0 = time.perf_counter()
+        codes, dig, _ = _sanitize(lib, [big])
+        dt = time.perf_counter() - t0
+        code, _, d = mr.sanitize(big, committee, sig)
+        assert codes[0] == code and dig[0].tobytes() == d
+        print("200k unsorted parents: %.1f ms" % (dt * 1e3))
+        assert dt < 2.0, dt
+    finally:
+        lib.nwc_set_committee(None, 0)

@@ -1,5 +1,5 @@
-"""The library's multi-device host paths on a one-GPU box: NWC_VIRTUAL_DEVICES=3 makes nwc_init open
-three contexts on the GPU, so nwc_verify_strict_many's shard threads and bitmap merge,
+"""The library's multi-device host paths on a one-GPU box: NWC_VIRTUAL_DEVICES=k (3, and 8 = one
+node's width) makes nwc_init open k contexts on the GPU, so nwc_verify_strict_many's shard threads and bitmap merge,
 nwc_verify_batch_many's certificate cuts and nwc_sha512_trunc32_many's split all run as with three
 GPUs.  Outputs must equal the oracle's bit for bit, including verdicts that
 straddle the shard boundaries."""
@@ -16,7 +16,8 @@ from tests.conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 
-def test_three_contexts_match_oracle(oracle, tmp_path):
+@pytest.mark.parametrize("contexts", [3, 8])
+def test_contexts_match_oracle(oracle, tmp_path, contexts):
     rng = np.random.default_rng(31)
     n = 9001                                        # > 4096: sharded; 9001 = not a multiple of 64
     seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
@@ -42,11 +43,11 @@ def test_three_contexts_match_oracle(oracle, tmp_path):
     blob = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
     boffs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
     np.savez(tmp_path / "in.npz", m=msgs, p=pks, s=sigs, offs=offs, dig=dig, blob=blob, boffs=boffs)
-    env = dict(os.environ, NWC_VIRTUAL_DEVICES="3")
+    env = dict(os.environ, NWC_VIRTUAL_DEVICES=str(contexts))
     subprocess.run([sys.executable, os.path.join(ROOT, "tests", "multidev_helper.py"), str(tmp_path / "in.npz"),
                     str(tmp_path / "out.npz"), ROOT], env=env, check=True, timeout=300)
     got = np.load(tmp_path / "out.npz")
-    assert int(got["devices"][0]) == 3
+    assert int(got["devices"][0]) == contexts
     bits = lambda raw, k: np.unpackbits(raw, bitorder="little")[:k].astype(bool)  # noqa: E731
     assert (bits(got["strict"], n) == oracle.strict_many(msgs, pks, sigs)).all()
     # batch: certificates over (vp, vs) -- rerun the helper's call shape against the oracle

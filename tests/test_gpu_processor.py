@@ -1,0 +1,96 @@
+"""The worker's Processor over the GPU batch digester (narwhal_amd/processor.py, nwc_digester_*):
+grouped digests against hashlib (the reference's Sha512::digest(&batch)[..32],
+worker/src/processor.rs:38), submission order and tags, grouping by max_group / max_wait_us, and
+the Processor's store writes and WorkerPrimaryMessage bytes on the reference's own batch fixture."""
+import hashlib
+import json
+import os
+import queue
+import struct
+import time
+
+import numpy as np
+import pytest
+
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _sha32(b) -> bytes:
+    return hashlib.sha512(bytes(b)).digest()[:32]
+
+
+def test_digester_groups_vs_hashlib():
+    from narwhal_amd.processor import Digester
+    rng = np.random.default_rng(5)
+    lens = [0, 1, 111, 112, 127, 128, 129, 239, 240, 255, 256] + [int(x) for x in rng.integers(0, 600_000, 60)]
+    batches = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    for max_group, wait in ((1, 0), (7, 0), (64, 200_000), (4096, 1000)):
+        dg = Digester(max_group, wait)
+        try:
+            tags = [dg.submit(b, 1000 + i) for i, b in enumerate(batches)]
+            got = []
+            t0 = time.time()
+            while len(got) < len(batches) and time.time() - t0 < 60:
+                got += dg.poll(4096, 100_000)
+            assert [t for t, _ in got] == tags            # submission order, caller's tags
+            for (t, d), b in zip(got, batches):
+                assert d == _sha32(b), (max_group, t, len(b))
+            groups, nb, nbytes = dg.stats()
+            assert nb == len(batches) and nbytes == sum(lens)
+            if max_group == 1:
+                assert groups == len(batches)
+            if max_group == 7:
+                assert groups >= (len(batches) + 6) // 7
+        finally:
+            dg.close()
+
+
+def test_digester_max_wait_gathers_a_burst():
+    """Everything submitted within max_wait of the first batch goes out in one launch."""
+    from narwhal_amd.processor import Digester
+    rng = np.random.default_rng(6)
+    batches = [rng.integers(0, 256, 5000, dtype=np.uint8).tobytes() for _ in range(50)]
+    dg = Digester(1024, 500_000)
+    try:
+        for b in batches:
+            dg.submit(b)
+        got = []
+        while len(got) < 50:
+            got += dg.poll(64, 1_000_000)
+        assert [d for _, d in got] == [_sha32(b) for b in batches]
+        assert dg.stats()[0] == 1
+    finally:
+        dg.close()
+
+
+def test_processor_reference_batch():
+    """Processor::spawn over the reference worker fixture (worker/src/tests/common.rs:87-109): the
+    digest, the store write under it, and bincode(WorkerPrimaryMessage::OurBatch(digest, id))."""
+    from narwhal_amd.processor import Processor, worker_primary_message
+    g = json.load(open(os.path.join(GOLDEN, "sha512.json")))
+    ref = [c for c in g["small"] if c.get("name") == "reference-serialized_batch"]
+    assert ref, "golden fixture missing"
+    batch = bytes.fromhex(ref[0]["msg"])
+    want = bytes.fromhex(ref[0]["digest32"])
+    assert _sha32(batch) == want
+
+    class Store(dict):
+        def write(self, k, v):
+            self[k] = v
+
+    rng = np.random.default_rng(7)
+    others = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(0, 100_000, 40)]
+    for own in (True, False):
+        store, rx, tx = Store(), queue.Queue(), queue.Queue()
+        p = Processor.spawn(3, store, rx, tx, own, max_group=16, max_wait_us=2000)
+        for b in [batch] + others:
+            rx.put(b)
+        rx.put(None)
+        p.join(60)
+        msgs = [tx.get_nowait() for _ in range(len(others) + 1)]
+        assert tx.empty()
+        assert msgs[0] == struct.pack("<I", 0 if own else 1) + want + struct.pack("<I", 3)
+        assert msgs[1:] == [worker_primary_message(_sha32(b), 3, own) for b in others]
+        assert store[want] == batch and len(store) == len({_sha32(b) for b in [batch] + others})
