@@ -89,9 +89,11 @@ class Processor:
     """`Processor::spawn(id, store, rx_batch, tx_digest, own_digest)` (processor.rs:22-34)."""
 
     def __init__(self, worker_id: int, store, rx_batch: "queue.Queue", tx_digest: "queue.Queue", own_digest: bool,
-                 max_group: int = 1024, max_wait_us: int = 1000):
+                 max_group: int = 1024, max_wait_us: int = 1000, digester=None):
         self.id, self.store, self.rx, self.tx, self.own = worker_id, store, rx_batch, tx_digest, own_digest
-        self.dg = Digester(max_group, max_wait_us)
+        # `digester` (submit/poll/close) is for host-logic unit tests only; the Processor itself
+        # always digests on the GPU (a missing libnwc raises here)
+        self.dg = digester if digester is not None else Digester(max_group, max_wait_us)
         self._pending: Dict[int, bytes] = {}
         self._submitted = 0
         self._done = 0

@@ -83,3 +83,56 @@ pub fn set_committee(public_keys: &[[u8; 32]]) {
     let pks: Vec<u8> = public_keys.iter().flat_map(|k| k.iter().copied()).collect();
     check(unsafe { ffi::nwc_set_committee(pks.as_ptr(), public_keys.len()) });
 }
+
+/// The worker's grouped batch digests (worker/src/processor.rs:35-55): a libnwc digester whose
+/// drain thread hashes whatever has queued up (up to `max_group` batches, or what arrived within
+/// `max_wait_us` of the first) in one GPU launch.  Batches are borrowed until their digest comes
+/// back, so the queue owns them here and hands each back with its digest, in submission order.
+pub struct BatchDigester {
+    q: *mut ffi::nwc_digester,
+    next_tag: u64,
+    held: std::collections::VecDeque<(u64, Vec<u8>)>,
+}
+
+unsafe impl Send for BatchDigester {}
+
+impl BatchDigester {
+    pub fn new(max_group: u32, max_wait_us: u32) -> Self {
+        init(0);
+        let q = unsafe { ffi::nwc_digester_create(max_group, max_wait_us) };
+        if q.is_null() {
+            let msg = unsafe { CStr::from_ptr(ffi::nwc_last_error()) };
+            panic!("libnwc digester: {}", msg.to_string_lossy());
+        }
+        BatchDigester { q, next_tag: 0, held: std::collections::VecDeque::new() }
+    }
+
+    /// Queue a batch (the Processor's `rx_batch.recv()`); it comes back from `next`.
+    pub fn submit(&mut self, batch: Vec<u8>) {
+        let tag = self.next_tag;
+        self.next_tag += 1;
+        check(unsafe { ffi::nwc_digester_submit(self.q, batch.as_ptr(), batch.len(), tag) });
+        self.held.push_back((tag, batch));   // the Vec's heap buffer does not move
+    }
+
+    /// The oldest outstanding batch with its digest, waiting up to `wait_us` (None on timeout).
+    pub fn next(&mut self, wait_us: u32) -> Option<([u8; 32], Vec<u8>)> {
+        if self.held.is_empty() {
+            return None;
+        }
+        let (mut tag, mut dig, mut n) = (0u64, [0u8; 32], 0usize);
+        check(unsafe { ffi::nwc_digester_poll(self.q, 1, wait_us, &mut tag, dig.as_mut_ptr(), &mut n) });
+        if n == 0 {
+            return None;
+        }
+        let (t, batch) = self.held.pop_front().unwrap();
+        assert_eq!(t, tag, "digests come back in submission order");
+        Some((dig, batch))
+    }
+}
+
+impl Drop for BatchDigester {
+    fn drop(&mut self) {
+        unsafe { ffi::nwc_digester_destroy(self.q) };
+    }
+}

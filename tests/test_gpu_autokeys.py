@@ -84,3 +84,31 @@ def test_random_certificates_with_bad_votes(lib):
             ok, bad = _batch(lib, D[c].tobytes(), P[c * q:(c + 1) * q].tobytes(), S[c * q:(c + 1) * q].tobytes(), q)
             assert bad == bad_sets[c], (c, sight)
             assert ok == (not bad_sets[c]), (c, sight)
+
+
+def test_lifecycle(tmp_path):
+    """NWC_AUTO_KEYS=4: the cache fills, new keys replace the oldest (FIFO) and take the latency
+    kernel, evicted keys fall back to the uncached path, nwc_set_committee empties it -- and every
+    verdict and bad set stays exact (crypto/src/lib.rs:206-219; config/src/lib.rs:154-156)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    out = tmp_path / "log.json"
+    env = dict(os.environ, NWC_AUTO_KEYS="4")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tests", "autokeys_lifecycle_helper.py"), ROOT, str(out)],
+                   env=env, check=True, timeout=300)
+    log = {e["tag"]: e for e in json.load(open(out))}
+    for e in log.values():
+        want_bad = 0 if e["corrupt"] is None else 1 << e["corrupt"]
+        assert e["rc"] == (0 if e["corrupt"] is None else 1) and e["bad"] == want_bad, e
+        assert e["cap"] == 4
+    assert log["A1"]["auto"] == 2 and log["A2"]["hits"] == log["A1"]["hits"] + 1
+    assert log["B1"]["auto"] == 4 and log["B2"]["hits"] == log["B1"]["hits"] + 1
+    assert log["C1"]["auto"] == 4 and log["C2"]["hits"] == log["C1"]["hits"] + 1      # replaced, then cached
+    assert log["A-after-eviction"]["hits"] == log["C2"]["hits"]                        # evicted: uncached path
+    assert log["C-cached"]["hits"] == log["C2"]["hits"] + 1
+    assert log["after-committee"]["auto"] == 0 and log["after-committee"]["committee"] == 2
+    assert log["after-committee"]["hits"] == log["C-cached"]["hits"]
+    assert log["C-again2"]["hits"] == log["C-again1"]["hits"] + 1 and log["C-again1"]["auto"] == 2

@@ -64,11 +64,13 @@ def test_golden_batches_straus(golden_batch):
     assert passes[[c for c, b in enumerate(batches) if b["class"] == "randomized"]].sum() > 0   # and its Ok outcome
 
 
-def test_certificates_vs_oracle(oracle):
-    """Honest and 1 %-bad certificates of many sizes (L = 1 .. 16 lanes per certificate, and one past
-    the Straus limit that takes the leaves): verdicts and bad sets equal the oracle's."""
+@pytest.mark.parametrize("big", [383, 1600])
+def test_certificates_vs_oracle(oracle, big):
+    """Honest and 1 %-bad certificates of many sizes: with a 383-vote certificate every launch splits
+    certificates over L = 16 lanes; with a 1,600-vote one (past 64 lanes x 24 votes) the call takes
+    the exact leaves.  Verdicts and bad sets equal the oracle's."""
     rng = np.random.default_rng(41)
-    sizes = [0, 1, 2, 3, 24, 25, 48, 49, 67, 67, 67, 100, 200, 383, 1600] + [int(x) for x in rng.integers(1, 90, 120)]
+    sizes = [0, 1, 2, 3, 24, 25, 48, 49, 67, 67, 67, 100, 200, big] + [int(x) for x in rng.integers(1, 90, 120)]
     m = len(sizes)
     offs = np.zeros(m + 1, np.int64)
     offs[1:] = np.cumsum(sizes)
