@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -1386,13 +1387,14 @@ int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, co
   uint32_t maxv = 0;
   HIP_TRY(hipMemcpyAsync(&maxv, d.straus_max, sizeof maxv, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  uint32_t L = 1;
-  while (L < 64 && (maxv + L - 1) / L > (uint32_t)nwc::STRAUS_MAX_PER_LANE) L <<= 1;
-  if (!d.comb16 || (maxv + L - 1) / L > (uint32_t)nwc::STRAUS_MAX_PER_LANE)
+  const uint64_t resident = (uint64_t)d.cus * 2 * 256;
+  uint32_t L = nwc::straus_lanes_per_cert(m, maxv, resident / 64);
+  if (const char* e = std::getenv("NWC_STRAUS_LANES")) L = (uint32_t)std::strtoul(e, nullptr, 10);   // A/B
+  if (!d.comb16 || L == 0 || L > 64 || (maxv + L - 1) / L > (uint32_t)nwc::STRAUS_MAX_PER_LANE)
     // no basepoint comb (NWC_COMB16=0) or certificates of > 1,536 votes: the exact leaves
     return launch_verify(d, dig, mi, 0, pks, sigs, nvotes, 0, leaf, s);
-  const uint64_t resident = (uint64_t)d.cus * 2 * 256;
-  const uint64_t lanes = std::min<uint64_t>((m * L + 255) / 256 * 256, resident);
+  const uint64_t need_waves = (m + 64 / L - 1) / (64 / L);
+  const uint64_t lanes = std::min<uint64_t>((need_waves * 64 + 255) / 256 * 256, resident);
   const uint64_t stride = (uint64_t)((maxv + L - 1) / L) * nwc::STRAUS_VOTE_BYTES;
   if (lanes * stride > d.straus_cap || (m + 63) / 64 > d.straus_cert_cap) {
     HIP_TRY(hipStreamSynchronize(s));

@@ -3,8 +3,9 @@
 //
 //     sum_i z_i R_i + sum_i (z_i k_i mod l) A_i - (sum_i z_i s_i mod l) B == O
 //
-// with random 128-bit z_i.  One certificate is split over L consecutive lanes (L a power of two,
-// chosen by the host so that each lane holds at most STRAUS_MAX_PER_LANE votes); lane q takes
+// with random 128-bit z_i.  One certificate is split over L consecutive lanes of a wave (L chosen
+// by the host, straus_lanes_per_cert, so that each lane holds at most STRAUS_MAX_PER_LANE votes
+// and the persistent grid's last round is nearly full); lane q takes
 // votes q, q + L, ... of its certificate and runs Straus over its 2 n_q points: the 63 x 4
 // doublings of its accumulator are shared by all of them, each window adds one entry per A_i
 // (signed radix-16 digits of z_i k_i mod l, 64 windows) and, in the low 33 windows, one per R_i
@@ -37,7 +38,7 @@ struct StrausArgs {
   const uint8_t* pks;         // nv x 32
   const uint8_t* sigs;        // nv x 64
   uint64_t m;
-  uint32_t lanes_per_cert;    // L: 1, 2, 4, ..., 64
+  uint32_t lanes_per_cert;    // L: 1 .. 64
   uint32_t seed[8];
   const ge_niels_pad* comb16; // radix-2^22 basepoint comb
   uint8_t* scratch;           // lane_stride bytes per lane slot
@@ -100,21 +101,32 @@ __device__ __forceinline__ i32 nib_digit(const u32* words, int w) {
   return (i32)((words[w >> 3] >> (4 * (w & 7))) & 15u) - 8;
 }
 
+// The digit words of the current 8 windows, per vote of each lane, staged in LDS every 8 windows
+// (row (2u + k) of 256 words, k = 0 the A digits, 1 the R digits; a wave's access is one 256-B row):
+// the ladder's digit reads then never wait on memory in front of their table gathers.
+constexpr int STRAUS_LDS_WORDS = 2 * STRAUS_MAX_PER_LANE * 256;
+
 __global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
-  const uint64_t lanes_total = (uint64_t)gridDim.x * blockDim.x;
+  __shared__ u32 dl[STRAUS_LDS_WORDS];
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const u32 L = a.lanes_per_cert;
-  const u32 q = threadIdx.x & (L - 1);
+  // groups of L consecutive lanes inside a wave (64 / L groups; the last 64 mod L lanes idle)
+  const u32 lane = threadIdx.x & 63;
+  const u32 gpw = 64u / L;
+  const u32 gi = lane / L;
+  const u32 q = lane - gi * L;
+  const bool in_group = gi < gpw;
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t groups = waves * gpw;
   uint8_t* const base = a.scratch + slot * a.lane_stride;
   // entry 0 (the identity) of the first vote's tables: the add every lane of a wave makes in a
   // (window, vote) step where it has no vote of its own reads it
   LaneTable{reinterpret_cast<uint4*>(base)}.store(0, ge_cached_identity());
   LaneTable{reinterpret_cast<uint4*>(base + TAB_BYTES_PER_LANE)}.store(0, ge_cached_identity());
-  // persistent: group g of L lanes takes certificates g, g + groups, ...
-  const uint64_t groups = lanes_total / L;
-  for (uint64_t c0 = slot / L; ; c0 += groups) {
+  // persistent: group g takes certificates g, g + groups, ...
+  for (uint64_t c0 = (slot >> 6) * gpw + gi; ; c0 += groups) {
     // wave-uniform loop exit: every lane of the wave leaves together
-    const bool active = c0 < a.m;
+    const bool active = in_group && c0 < a.m;
     if (!__any(active)) break;
     const uint64_t c = active ? c0 : 0;
     const uint32_t o0 = active ? a.voffs[c] : 0, o1 = active ? a.voffs[c + 1] : 0;
@@ -171,30 +183,48 @@ __global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
     _Pragma("unroll") for (int msk = 32; msk >= 1; msk >>= 1) nw = max(nw, (uint32_t)__shfl_xor((int)nw, msk, 64));
 #pragma unroll 1
     for (int w = 63; w >= 0; --w) {
+      if ((w & 7) == 7) {
+        // stage the next 8 windows' digit words (a lane without vote u stages digit 0 = +8 nibbles)
+#pragma unroll 1
+        for (uint32_t u = 0; u < nw; ++u) {
+          const u32* dg = reinterpret_cast<const u32*>(base + (size_t)u * STRAUS_VOTE_BYTES + 2 * TAB_BYTES_PER_LANE);
+          const bool has = u < nq;
+          dl[(2 * u) * 256 + threadIdx.x] = has ? dg[w >> 3] : 0x88888888u;
+          dl[(2 * u + 1) * 256 + threadIdx.x] = has ? dg[8 + (w >> 3)] : 0x88888888u;
+        }
+      }
       if (w != 63) ladder_dbl4(t);
+      const int sh = 4 * (w & 7);
 #pragma unroll 1
       for (uint32_t u = 0; u < nw; ++u) {
-        const bool has = u < nq;
-        uint8_t* vb = base + (size_t)(has ? u : 0) * STRAUS_VOTE_BYTES;
-        const u32* dg = reinterpret_cast<const u32*>(vb + 2 * TAB_BYTES_PER_LANE);
-        const i32 da = has ? nib_digit(dg, w) : 0;
+        uint8_t* vb = base + (size_t)(u < nq ? u : 0) * STRAUS_VOTE_BYTES;
+        const i32 da = (i32)((dl[(2 * u) * 256 + threadIdx.x] >> sh) & 15u) - 8;
         t = add_lt(t, LaneTable{reinterpret_cast<uint4*>(vb)}, da < 0 ? -da : da, da < 0);
         if (w <= 32) {
-          const i32 dr = has ? nib_digit(dg + 8, w) : 0;
+          const i32 dr = (i32)((dl[(2 * u + 1) * 256 + threadIdx.x] >> sh) & 15u) - 8;
           t = add_lt(t, LaneTable{reinterpret_cast<uint4*>(vb + TAB_BYTES_PER_LANE)}, dr < 0 ? -dr : dr, dr < 0);
         }
       }
     }
-    // ---- phase 3: the group's partial sums, -S B, identity test
+    // ---- phase 3: the group's partial sums (a segmented tree towards q = 0), -S B, identity test
     ge_p3 P = ge_p1p1_to_p3(t);
 #pragma unroll 1
-    for (u32 msk = 1; msk < L; msk <<= 1) {
-      const ge_p3 Q = shfl_xor_p3w(P, (int)msk);
-      P = ge_p1p1_to_p3(ge_add_cached(P, ge_p3_to_cached(Q)));
+    for (u32 off = 1; off < L; off <<= 1) {
+      ge_p3 Q;
+      {
+        const fe* sp = &P.X;
+        fe* dp = &Q.X;
+        _Pragma("unroll") for (int k = 0; k < 4; ++k)
+          _Pragma("unroll") for (int i = 0; i < 10; ++i) dp[k].v[i] = __shfl_down(sp[k].v[i], off, 64);
+      }
       u32 So[8];
-      _Pragma("unroll") for (int i = 0; i < 8; ++i) So[i] = (u32)__shfl_xor((int)S[i], (int)msk, 64);
-      sc_add_l(S, So, S);
-      ok = ok && (__shfl_xor((int)ok, (int)msk, 64) != 0);
+      _Pragma("unroll") for (int i = 0; i < 8; ++i) So[i] = (u32)__shfl_down((int)S[i], off, 64);
+      const bool oko = __shfl_down((int)ok, off, 64) != 0;
+      if ((q & (2 * off - 1)) == 0 && q + off < L) {
+        P = ge_p1p1_to_p3(ge_add_cached(P, ge_p3_to_cached(Q)));
+        sc_add_l(S, So, S);
+        ok = ok && oko;
+      }
     }
     // -S = l - S (S < l; S = 0 stays 0)
     u32 nS[8];
@@ -220,6 +250,27 @@ __global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
     if (active && q == 0 && ok && ident)
       atomicOr(reinterpret_cast<unsigned long long*>(a.cert_words) + (c >> 6), 1ull << (c & 63));
   }
+}
+
+// Lanes per certificate for k_verify_straus: each lane pays ~252 doublings whatever it holds, and
+// a persistent grid of G groups gives each group ceil(m / G) certificates in turn, so the
+// last round can be nearly empty.  The host picks the L in 1..64 (any, not only powers of two)
+// that minimises (per-vote work + the doublings' share) / (round efficiency x lanes used), with
+// at most STRAUS_MAX_PER_LANE votes per lane.  Work in units of ~1k VALU instructions per vote.
+inline uint32_t straus_lanes_per_cert(uint64_t m, uint32_t maxv, uint64_t resident_waves) {
+  uint32_t best = 0;
+  double best_cost = 1e300;
+  for (uint32_t L = 1; L <= 64; ++L) {
+    const uint32_t nq = (maxv + L - 1) / L;
+    if (nq > (uint32_t)STRAUS_MAX_PER_LANE) continue;
+    const uint32_t gpw = 64 / L;
+    const double groups = (double)resident_waves * gpw;
+    const double rounds = (double)m / groups;
+    const double eff = (rounds / std::ceil(rounds)) * (double)(gpw * L) / 64.0;
+    const double cost = (230.0 + 245.0 / (double)(nq ? nq : 1)) / eff;
+    if (cost < best_cost) { best_cost = cost; best = L; }
+  }
+  return best;
 }
 
 // Largest certificate (votes) of a launch: one atomicMax per certificate (L is chosen from it).
