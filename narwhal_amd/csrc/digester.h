@@ -8,8 +8,9 @@
 // one launch.  Results come back in submission order.
 //
 // Data path per group: the borrowed batches are gathered into two pinned 64-MB stages in turn
-// (16-byte-aligned starts, the kernel's dwordx4 path) and copied on the digester's own stream into
-// one device buffer while the next stage is filled; then k_sha512_digest32[_sched] over the group
+// (16-byte-aligned starts, the kernel's dwordx4 path; each stage filled by up to 8 host threads, as
+// one memcpy thread moves only ~10 GB/s) and DMA'd on the digester's own stream into one device
+// buffer while the next stage is filled; then k_sha512_digest32[_sched] over the group
 // and one D2H of 32 bytes per batch.  The digester has its own stream and buffers (it does not
 // serialise with verification calls on the device's context).  Included by nwc_api.hip.
 #pragma once
@@ -23,6 +24,7 @@ struct Digester {
   struct Item { const uint8_t* p; size_t len; uint64_t tag; };
   uint32_t max_group, max_wait_us;
   int hip_id;
+  unsigned copy_threads = 8;        // host threads filling a pinned stage (NWC_DIGEST_COPY_THREADS)
   std::mutex mu;
   std::condition_variable cv_in, cv_out;
   std::deque<Item> in;
@@ -50,7 +52,9 @@ struct Digester {
     HIP_TRY(hipSetDevice(hip_id));
     HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (int s = 0; s < 2; ++s) {
-      HIP_TRY(hipHostMalloc(&stage[s], STAGE, hipHostMallocDefault));
+      // non-coherent: ordinary cached host pages for the copy threads (the default, fine-grained
+      // kind is uncached for CPU stores and caps the gather at a few GB/s); the DMA reads it
+      HIP_TRY(hipHostMalloc(&stage[s], STAGE, hipHostMallocNonCoherent));
       HIP_TRY(hipEventCreateWithFlags(&stage_ev[s], hipEventDisableTiming));
     }
     return 0;
@@ -100,40 +104,42 @@ struct Digester {
       HIP_TRY(hipMalloc(&ddata, cap));
       ddata_cap = cap;
     }
-    // gather through the two pinned stages: fill one while the other's copy is in flight
+    // gather through the two pinned stages: fill one (with copy_threads host threads, each a
+    // contiguous byte range of the stage) while the other's DMA is in flight.  Stage s covers the
+    // device layout's bytes [pos, pos + STAGE); batch i sits at hse[i] (16-byte aligned starts).
     int s = 0;
-    size_t fill = 0;
-    uint64_t dst = 0;   // device offset of the stage's first byte
     bool used[2] = {false, false};
-    auto flush = [&]() -> int {
-      if (fill == 0) return 0;
-      HIP_TRY(hipMemcpyAsync(ddata + dst, stage[s], fill, hipMemcpyHostToDevice, stream));
+    size_t first = 0;   // first batch that may overlap the current stage
+    for (uint64_t pos = 0; pos < total; pos += STAGE) {
+      const uint64_t end = std::min<uint64_t>(pos + STAGE, total);
+      if (used[s]) HIP_TRY(hipEventSynchronize(stage_ev[s]));   // its previous DMA has landed
+      while (first < k && hse[k + first] <= pos) ++first;   // batches wholly in earlier stages
+      auto copy_range = [&](uint64_t lo, uint64_t hi) {
+        // batches overlapping [lo, hi), found from `first` (starts are ascending)
+        size_t i = first;
+        while (i < k && hse[k + i] <= lo) ++i;
+        for (; i < k && hse[i] < hi; ++i) {
+          const uint64_t a0 = std::max<uint64_t>(hse[i], lo), a1 = std::min<uint64_t>(hse[k + i], hi);
+          if (a1 > a0) std::memcpy(stage[s] + (a0 - pos), g[i].p + (a0 - hse[i]), a1 - a0);
+        }
+      };
+      const uint64_t bytes = end - pos;
+      const unsigned nt = (unsigned)std::min<uint64_t>(copy_threads, (bytes + (4u << 20) - 1) / (4u << 20));
+      if (nt <= 1) {
+        copy_range(pos, end);
+      } else {
+        std::vector<std::thread> th;
+        const uint64_t per = (bytes + nt - 1) / nt;
+        for (unsigned t = 1; t < nt; ++t)
+          th.emplace_back(copy_range, pos + t * per, std::min<uint64_t>(end, pos + (t + 1) * per));
+        copy_range(pos, std::min<uint64_t>(end, pos + per));
+        for (auto& x : th) x.join();
+      }
+      HIP_TRY(hipMemcpyAsync(ddata + pos, stage[s], bytes, hipMemcpyHostToDevice, stream));
       HIP_TRY(hipEventRecord(stage_ev[s], stream));
       used[s] = true;
-      dst += fill;
-      fill = 0;
       s ^= 1;
-      if (used[s]) HIP_TRY(hipEventSynchronize(stage_ev[s]));   // its previous copy has landed
-      return 0;
-    };
-    for (size_t i = 0; i < k; ++i) {
-      const uint8_t* p = g[i].p;
-      size_t left = g[i].len;
-      const size_t padded = (g[i].len + 15) & ~(size_t)15;
-      size_t pad = padded - g[i].len;
-      while (left) {
-        const size_t c = std::min(left, STAGE - fill);
-        std::memcpy(stage[s] + fill, p, c);
-        fill += c; p += c; left -= c;
-        if (fill == STAGE) if (int rc = flush()) return rc;
-      }
-      while (pad) {   // alignment gap (never read by the kernel)
-        const size_t c = std::min(pad, STAGE - fill);
-        fill += c; pad -= c;
-        if (fill == STAGE) if (int rc = flush()) return rc;
-      }
     }
-    if (int rc = flush()) return rc;
     HIP_TRY(hipMemcpyAsync(dse, hse, 16 * k, hipMemcpyHostToDevice, stream));
     if (int rc = launch_digest(ddata, dse, dse + k, k, dout, stream)) return rc;
     HIP_TRY(hipMemcpyAsync(hout, dout, 32 * k, hipMemcpyDeviceToHost, stream));
@@ -197,6 +203,7 @@ nwc_digester* nwc_digester_create(uint32_t max_group, uint32_t max_wait_us) {
   q->max_group = max_group;
   q->max_wait_us = max_wait_us;
   q->hip_id = ctx(t_dev < (int)g_devs.size() ? t_dev : 0)->hip_id;
+  if (const char* e = std::getenv("NWC_DIGEST_COPY_THREADS")) q->copy_threads = std::max(1, std::atoi(e));
   if (q->init()) {
     q->release();
     delete q;

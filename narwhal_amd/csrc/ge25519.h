@@ -34,6 +34,18 @@ FE_DEV ge_p2 ge_p1p1_to_p2(const ge_p1p1& p) {
 FE_DEV ge_p3 ge_p1p1_to_p3(const ge_p1p1& p) {
   ge_p3 r; r.X = fe_mul(p.X, p.T); r.Y = fe_mul(p.Y, p.Z); r.Z = fe_mul(p.Z, p.T); r.T = fe_mul(p.X, p.Y); return r;
 }
+// The same conversions for a completed point whose Y is the sum of two tight elements (the output
+// of ge_p2_dbl, of the cached/Niels additions, or of a re-centred table entry -- the ladders'
+// accumulator): fe_mul(f, g) prepares 2 f_i (odd i) and 19 g_j once per distinct operand, so with
+// Y on the right the four products share two f's (X, Z) and two g's (T, Y): 9 v_mul_lo_u32 and 5
+// shifts fewer than (X.T, Y.Z, Z.T, X.Y).  Y as a right operand needs |19 Y_j| < 2^31, which a
+// sum of two tight elements meets (2^30.3) and 2y from an unreduced Niels entry does not.
+FE_DEV ge_p2 ge_p1p1_to_p2_acc(const ge_p1p1& p) {
+  ge_p2 r; r.X = fe_mul(p.X, p.T); r.Y = fe_mul(p.Z, p.Y); r.Z = fe_mul(p.Z, p.T); return r;
+}
+FE_DEV ge_p3 ge_p1p1_to_p3_acc(const ge_p1p1& p) {
+  ge_p3 r; r.X = fe_mul(p.X, p.T); r.Y = fe_mul(p.Z, p.Y); r.Z = fe_mul(p.Z, p.T); r.T = fe_mul(p.X, p.Y); return r;
+}
 FE_DEV ge_p2 ge_p3_to_p2(const ge_p3& p) { ge_p2 r; r.X = p.X; r.Y = p.Y; r.Z = p.Z; return r; }
 FE_DEV ge_cached ge_p3_to_cached(const ge_p3& p) {
   ge_cached r; r.YpX = fe_add(p.Y, p.X); r.YmX = fe_sub(p.Y, p.X); r.Z = p.Z; r.T2d = fe_mul(p.T, FE_D2); return r;

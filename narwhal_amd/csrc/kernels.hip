@@ -511,7 +511,7 @@ __device__ __forceinline__ ge_cached lt_first(const LaneTable& tab, int e) {
 __device__ __forceinline__ ge_p1p1 add_lt(const ge_p1p1& t, const LaneTable& tab, int e, bool neg) {
   const fe qa = lt_load_fe(tab, e, neg ? 1 : 0);
   const fe qb = lt_load_fe(tab, e, neg ? 0 : 1);
-  const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Y, t.Z);
+  const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Z, t.Y);
   const fe a = fe_add(Y3, X3), b = fe_sub(Y3, X3);
   const fe Z3 = fe_mul(t.Z, t.T), T3 = fe_mul(t.X, t.Y);
 #if NWC_ADD_LT_SPLIT
@@ -531,6 +531,39 @@ __device__ __forceinline__ ge_p1p1 add_lt(const ge_p1p1& t, const LaneTable& tab
   r.T = fe_sub(zz2, tt);
   return r;
 }
+
+#if NWC_PACKED_TABLES
+// add_lt with the entry's first two coordinates (Y+X, Y-X, swapped when neg) already loaded --
+// packed, 4 x uint4 -- so a caller that knows its next digit can issue the gather one addition
+// ahead (k_verify_straus: consecutive additions with no doubling between them).
+__device__ __forceinline__ void lt_load_ab(const LaneTable& tab, int e, bool neg, uint4 ab[4]) {
+  const int ka = neg ? 1 : 0, kb = neg ? 0 : 1;
+  ab[0] = tab.p[e * 8 + 2 * ka];
+  ab[1] = tab.p[e * 8 + 2 * ka + 1];
+  ab[2] = tab.p[e * 8 + 2 * kb];
+  ab[3] = tab.p[e * 8 + 2 * kb + 1];
+}
+__device__ __forceinline__ ge_p1p1 add_lt_ab(const ge_p1p1& t, const uint4 ab[4], const LaneTable& tab, int e,
+                                             bool neg) {
+  const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Z, t.Y);
+  const fe a = fe_add(Y3, X3), b = fe_sub(Y3, X3);
+  const fe Z3 = fe_mul(t.Z, t.T), T3 = fe_mul(t.X, t.Y);
+  __builtin_amdgcn_sched_barrier(0);
+  const fe qz = lt_load_fe(tab, e, 2);
+  const fe qt = lt_load_fe(tab, e, 3);
+  const fe pp = fe_mul(a, fe_unpack(ab[0], ab[1])), mm = fe_mul(b, fe_unpack(ab[2], ab[3]));
+  ge_p1p1 r;
+  r.X = fe_sub(pp, mm);
+  r.Y = fe_add(pp, mm);
+  const fe zz = fe_mul(Z3, qz);
+  const fe zz2 = fe_add(zz, zz);
+  fe tt = fe_mul(T3, qt);
+  tt = fe_select(tt, fe_neg(tt), neg);
+  r.Z = fe_add(zz2, tt);
+  r.T = fe_sub(zz2, tt);
+  return r;
+}
+#endif
 
 // tab[j] = j * P for j = 0..8 (tab[0] = identity)
 __device__ __forceinline__ void build_table(const LaneTable& tab, const ge_p3& P) {
@@ -779,9 +812,9 @@ __device__ __forceinline__ ge_p1p1 ge_cached_to_p1p1(const ge_cached& c) {
 
 // four doublings of t (t in, t out), (X:Y:Z) only
 __device__ __forceinline__ void ladder_dbl4(ge_p1p1& t) {
-  ge_p2 p2 = ge_p1p1_to_p2(t);
+  ge_p2 p2 = ge_p1p1_to_p2_acc(t);
 #pragma unroll 1
-  for (int j = 0; j < 3; ++j) { t = ge_p2_dbl(p2); p2 = ge_p1p1_to_p2(t); }
+  for (int j = 0; j < 3; ++j) { t = ge_p2_dbl(p2); p2 = ge_p1p1_to_p2_acc(t); }
   t = ge_p2_dbl(p2);
 }
 
@@ -816,7 +849,7 @@ __device__ __forceinline__ void base_adds(ge_p1p1& t, int nb, i32 d0, i32 d1, ui
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): entry 0 is in VGPRs before the slot is reused
         stage_fetch(stage, 0, T24 + B24_ENTRIES + (d1 < 0 ? -d1 : d1));
       }
-      t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(e, dd_ < 0));
+      t = ge_add_niels(ge_p1p1_to_p3_acc(t), ge_niels_cneg(e, dd_ < 0));
       if (NWC_STAGE_ENTRIES == 1 && side + 1 < nb) stage_wait();
     }
   }
@@ -917,8 +950,8 @@ __device__ __forceinline__ ge_p2 half_scalarmult_cached(const LaneTable& tr, Dig
     if (w != W - 1) ladder_dbl4(t);
     i32 d0 = 0, d1 = 0;
     const int nb = base_fetch(w, bd, d0, d1, T24, stage);
-    if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
-    if ((w & 1) == 0) t = ge_add_niels(ge_p1p1_to_p3(t), ge_niels_cneg(ean, (dA < 0) != c_neg));
+    if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3_acc(t), ge_cached_cneg(er, dr < 0));
+    if ((w & 1) == 0) t = ge_add_niels(ge_p1p1_to_p3_acc(t), ge_niels_cneg(ean, (dA < 0) != c_neg));
     base_adds(t, nb, d0, d1, stage, T24);
     if (w > 0) {
       dr = next16(dd);

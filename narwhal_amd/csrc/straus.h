@@ -195,16 +195,41 @@ __global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
       }
       if (w != 63) ladder_dbl4(t);
       const int sh = 4 * (w & 7);
+      // the window's additions in order A_0, R_0, A_1, R_1, ... (R only in the low 33 windows):
+      // addition j = (vote j / per, kind j % per); each one's first gather is issued an addition ahead
+      const uint32_t per = w <= 32 ? 2u : 1u, nadd = nw * per;
+      auto entry = [&](uint32_t j, i32& d, LaneTable& tab) {
+        const uint32_t u = j / per, kind = j - u * per;
+        tab = LaneTable{reinterpret_cast<uint4*>(base + (size_t)(u < nq ? u : 0) * STRAUS_VOTE_BYTES +
+                                                 kind * TAB_BYTES_PER_LANE)};
+        d = (i32)((dl[(2 * u + kind) * 256 + threadIdx.x] >> sh) & 15u) - 8;
+      };
+#if NWC_PACKED_TABLES
+      i32 dn;
+      LaneTable tn;
+      entry(0, dn, tn);
+      uint4 ab[4];
+      lt_load_ab(tn, dn < 0 ? -dn : dn, dn < 0, ab);
 #pragma unroll 1
-      for (uint32_t u = 0; u < nw; ++u) {
-        uint8_t* vb = base + (size_t)(u < nq ? u : 0) * STRAUS_VOTE_BYTES;
-        const i32 da = (i32)((dl[(2 * u) * 256 + threadIdx.x] >> sh) & 15u) - 8;
-        t = add_lt(t, LaneTable{reinterpret_cast<uint4*>(vb)}, da < 0 ? -da : da, da < 0);
-        if (w <= 32) {
-          const i32 dr = (i32)((dl[(2 * u + 1) * 256 + threadIdx.x] >> sh) & 15u) - 8;
-          t = add_lt(t, LaneTable{reinterpret_cast<uint4*>(vb + TAB_BYTES_PER_LANE)}, dr < 0 ? -dr : dr, dr < 0);
+      for (uint32_t j = 0; j < nadd; ++j) {
+        const i32 d = dn;
+        const LaneTable tab = tn;
+        uint4 cur[4] = {ab[0], ab[1], ab[2], ab[3]};
+        if (j + 1 < nadd) {
+          entry(j + 1, dn, tn);
+          lt_load_ab(tn, dn < 0 ? -dn : dn, dn < 0, ab);
         }
+        t = add_lt_ab(t, cur, tab, d < 0 ? -d : d, d < 0);
       }
+#else
+#pragma unroll 1
+      for (uint32_t j = 0; j < nadd; ++j) {
+        i32 d;
+        LaneTable tab;
+        entry(j, d, tab);
+        t = add_lt(t, tab, d < 0 ? -d : d, d < 0);
+      }
+#endif
     }
     // ---- phase 3: the group's partial sums (a segmented tree towards q = 0), -S B, identity test
     ge_p3 P = ge_p1p1_to_p3(t);

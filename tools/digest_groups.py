@@ -59,7 +59,11 @@ def main():
     want = [hashlib.sha512(b).digest()[:32] for b in pool]
     th = cpu_threads()
     res = {"batch_bytes": BATCH, "pool_distinct": args.pool, "cpu_threads": th, "rows": []}
-    dev_pool = torch.frombuffer(bytearray(b"".join(pool)), dtype=torch.uint8).cuda()
+    STRIDE = (BATCH + 255) & ~255   # resident batches start 256-B aligned (the kernel's dwordx4 path)
+    flat = bytearray(STRIDE * args.pool)
+    for i, b in enumerate(pool):
+        flat[i * STRIDE:i * STRIDE + BATCH] = b
+    dev_pool = torch.frombuffer(flat, dtype=torch.uint8).cuda()
     for G in [int(x) for x in args.groups.split(",")]:
         row = {"group": G, "bytes": G * BATCH}
         # --- the Processor path from host memory
@@ -81,7 +85,7 @@ def main():
         row["gpu_digester"] = {"latency_ms": dt * 1e3, "GBps": G * BATCH / dt / 1e9, "submit_ms": t_sub * 1e3,
                                "groups_total": groups, "parity_ok": True}
         # --- resident in HBM: the kernel alone
-        starts = torch.tensor([(i % args.pool) * BATCH for i in range(G)], dtype=torch.int64, device="cuda")
+        starts = torch.tensor([(i % args.pool) * STRIDE for i in range(G)], dtype=torch.int64, device="cuda")
         ends = starts + BATCH
         out = torch.empty((G, 32), dtype=torch.uint8, device="cuda")
         s = torch.cuda.current_stream()
