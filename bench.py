@@ -393,7 +393,7 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
         cert_ok = torch.from_numpy(device.unpack_bits(cw, m)).cuda()
         ok = ok and bool((cert_ok == ~want_bad.view(m, Q).any(dim=1)).all())
         out[tag] = {"votes_per_s": nv / dt, "certs_per_s": m / dt, "ms_per_step": dt * 1e3, "parity_ok": ok,
-                    "equation": "dalek batch equation per certificate (Straus), leaves for failing ones"
+                    "equation": "dalek batch equation over sub-batches of ~12 votes (Straus per lane), leaves for failing sub-batches"
                     if eq == "straus" else "per-vote leaves", "bad_rate": 0.01 if want_bad is bad else 0.0}
     _lib.check(lib.nwc_set_committee(None, 0))
     if cpu_budget > 0:

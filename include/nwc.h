@@ -168,15 +168,17 @@ int nwc_dev_verify(const void* d_msgs, const void* d_msg_index, uint64_t msg_str
 int nwc_dev_cert_reduce(const void* d_leaf_words, const void* d_offsets, uint64_t m, uint64_t nvotes,
                         void* d_cert_words, void* d_bad_words, void* stream);
 /* Signature::verify_batch over m certificates as dalek's own batch equation (crypto/src/lib.rs:
- * 206-219; ed25519-dalek 1.0.1 batch.rs): per certificate, sum z_i R_i + sum (z_i k_i mod l) A_i -
- * (sum z_i s_i mod l) B == O with random 128-bit z_i, one Straus pass with shared doublings
- * (k_verify_straus); the votes of certificates it rejects are then re-decided by the exact
+ * 206-219; ed25519-dalek 1.0.1 batch.rs) over sub-batches of ~12 consecutive votes (any
+ * certificates; NWC_STRAUS_NQ overrides): sum z_i R_i + sum (z_i k_i mod l) A_i -
+ * (sum z_i s_i mod l) B == O with random 128-bit z_i, one Straus pass with shared doublings per
+ * lane (k_verify_straus); the votes of sub-batches it rejects are then re-decided by the exact
  * per-vote leaves, so d_leaf_words (a bit per vote, as nwc_dev_verify's) feeds nwc_dev_cert_reduce
- * for the certificate verdicts and the exact bad-vote set.  d_offsets: m + 1 uint32 vote offsets;
- * d_msg_index: the certificate of each vote.  Same verdicts as the leaf path on the deterministic
- * domain; on dalek's randomized domain (pure-torsion residuals, torsion-bearing keys) a
- * certificate passes with dalek's probability (~1/ord) where the leaf path answers Err.  Without
- * the basepoint comb (NWC_COMB16=0) or for certificates of > 1,536 votes it runs the leaves. */
+ * for the certificate verdicts and the exact bad-vote set.  d_offsets: m + 1 uint32 vote offsets
+ * (checked non-null; the sub-batches do not follow them); d_msg_index: the certificate of each
+ * vote.  Same verdicts and bad sets as the leaf path on the deterministic domain; on dalek's
+ * randomized domain (pure-torsion residuals, torsion-bearing keys) a vote's sub-batch passes with
+ * dalek's probability (~1/ord) where the leaf path answers Err.  Without the basepoint comb
+ * (NWC_COMB16=0) it runs the leaves. */
 int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, const void* d_msg_index, uint64_t m,
                                 uint64_t nvotes, const void* d_pks, const void* d_sigs, void* d_leaf_words,
                                 void* stream);

@@ -563,6 +563,33 @@ __device__ __forceinline__ ge_p1p1 add_lt_ab(const ge_p1p1& t, const uint4 ab[4]
   r.T = fe_sub(zz2, tt);
   return r;
 }
+// The whole packed entry (Y+X, Y-X swapped when neg, Z, 2dT: 8 x uint4) gathered ahead of its
+// add, so that the add issues no load of its own: with a partial prefetch the add's own Z / 2dT
+// loads were the newest in flight, and the in-order vmcnt wait for them also waited for the next
+// entry's prefetch (k_verify_straus: consecutive additions with no doubling between them).
+__device__ __forceinline__ void lt_load_full(const LaneTable& tab, int e, bool neg, uint4 q[8]) {
+  lt_load_ab(tab, e, neg, q);
+  q[4] = tab.p[e * 8 + 4];
+  q[5] = tab.p[e * 8 + 5];
+  q[6] = tab.p[e * 8 + 6];
+  q[7] = tab.p[e * 8 + 7];
+}
+__device__ __forceinline__ ge_p1p1 add_lt_full(const ge_p1p1& t, const uint4 q[8], bool neg) {
+  const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Z, t.Y);
+  const fe a = fe_add(Y3, X3), b = fe_sub(Y3, X3);
+  const fe Z3 = fe_mul(t.Z, t.T), T3 = fe_mul(t.X, t.Y);
+  const fe pp = fe_mul(a, fe_unpack(q[0], q[1])), mm = fe_mul(b, fe_unpack(q[2], q[3]));
+  ge_p1p1 r;
+  r.X = fe_sub(pp, mm);
+  r.Y = fe_add(pp, mm);
+  const fe zz = fe_mul(Z3, fe_unpack(q[4], q[5]));
+  const fe zz2 = fe_add(zz, zz);
+  fe tt = fe_mul(T3, fe_unpack(q[6], q[7]));
+  tt = fe_select(tt, fe_neg(tt), neg);
+  r.Z = fe_add(zz2, tt);
+  r.T = fe_sub(zz2, tt);
+  return r;
+}
 #endif
 
 // tab[j] = j * P for j = 0..8 (tab[0] = identity)

@@ -122,9 +122,6 @@ struct DevCtx {
   int comb_blocks_per_cu = 1;
   uint8_t* straus_scratch = nullptr;   // k_verify_straus per-lane tables (nwc_dev_verify_batch_straus)
   size_t straus_cap = 0;
-  uint64_t* straus_cert = nullptr;     // its certificate verdict words
-  size_t straus_cert_cap = 0;
-  uint32_t* straus_max = nullptr;      // largest certificate of the launch
   uint32_t* uc_list = nullptr;     // k_verify_comb: equations whose key is not cached
   uint32_t* uc_count = nullptr;
   // k_verify per-lane table slots; reused by every launch, so launches that use it are
@@ -1065,8 +1062,6 @@ void nwc_shutdown(void) {
     if (d->comb16_bases) (void)hipFree(d->comb16_bases);
     if (d->kb_bases) (void)hipFree(d->kb_bases);
     if (d->straus_scratch) (void)hipFree(d->straus_scratch);
-    if (d->straus_cert) (void)hipFree(d->straus_cert);
-    if (d->straus_max) (void)hipFree(d->straus_max);
     if (d->pinned) (void)hipHostFree(d->pinned);
     if (d->cc_stakes) (void)hipFree(d->cc_stakes);
     if (d->cc_worker_off) (void)hipFree(d->cc_worker_off);
@@ -1379,59 +1374,42 @@ int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, co
   const auto* pks = static_cast<const uint8_t*>(d_pks);
   const auto* sigs = static_cast<const uint8_t*>(d_sigs);
   auto* leaf = static_cast<uint64_t*>(d_leaf_words);
-  // the largest certificate decides how many lanes share one (each lane holds <= 24 votes)
-  if (!d.straus_max) HIP_TRY(hipMalloc(&d.straus_max, sizeof(uint32_t)));
-  HIP_TRY(hipMemsetAsync(d.straus_max, 0, sizeof(uint32_t), s));
-  hipLaunchKernelGGL(nwc::k_cert_maxlen, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, voffs, m, d.straus_max);
-  HIP_TRY(hipGetLastError());
-  uint32_t maxv = 0;
-  HIP_TRY(hipMemcpyAsync(&maxv, d.straus_max, sizeof maxv, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  const uint64_t resident = (uint64_t)d.cus * 2 * 256;
-  uint32_t L = nwc::straus_lanes_per_cert(m, maxv, resident / 64);
-  if (const char* e = std::getenv("NWC_STRAUS_LANES")) L = (uint32_t)std::strtoul(e, nullptr, 10);   // A/B
-  if (!d.comb16 || L == 0 || L > 64 || (maxv + L - 1) / L > (uint32_t)nwc::STRAUS_MAX_PER_LANE)
-    // no basepoint comb (NWC_COMB16=0) or certificates of > 1,536 votes: the exact leaves
+  if (!d.comb16)   // no basepoint comb (NWC_COMB16=0): the exact leaves
     return launch_verify(d, dig, mi, 0, pks, sigs, nvotes, 0, leaf, s);
-  const uint64_t need_waves = (m + 64 / L - 1) / (64 / L);
-  const uint64_t lanes = std::min<uint64_t>((need_waves * 64 + 255) / 256 * 256, resident);
-  const uint64_t stride = (uint64_t)((maxv + L - 1) / L) * nwc::STRAUS_VOTE_BYTES;
-  if (lanes * stride > d.straus_cap || (m + 63) / 64 > d.straus_cert_cap) {
+  (void)voffs;
+  // sub-batches of ~NWC_STRAUS_NQ votes (default 12), every lane slot the same number of rounds
+  uint32_t target = 12;
+  if (const char* e = std::getenv("NWC_STRAUS_NQ")) target = (uint32_t)std::strtoul(e, nullptr, 10);   // A/B
+  const uint64_t resident = (uint64_t)d.cus * nwc::STRAUS_WAVES_PER_SIMD * 256;
+  const uint64_t runs = nwc::straus_runs(nvotes, resident, target);
+  const uint64_t lanes = std::min<uint64_t>((runs + 255) / 256 * 256, resident);
+  const uint64_t maxq = (nvotes + runs - 1) / runs;
+  const uint64_t stride = maxq * nwc::STRAUS_VOTE_BYTES;
+  if (lanes * stride > d.straus_cap) {
     HIP_TRY(hipStreamSynchronize(s));
-    if (lanes * stride > d.straus_cap) {
-      if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
-      d.straus_scratch = nullptr;
-      d.straus_cap = 0;
-      HIP_TRY(hipMalloc(&d.straus_scratch, lanes * stride));
-      d.straus_cap = lanes * stride;
-    }
-    if ((m + 63) / 64 > d.straus_cert_cap) {
-      if (d.straus_cert) HIP_TRY(hipFree(d.straus_cert));
-      d.straus_cert = nullptr;
-      d.straus_cert_cap = 0;
-      HIP_TRY(hipMalloc(&d.straus_cert, 8 * ((m + 63) / 64)));
-      d.straus_cert_cap = (m + 63) / 64;
-    }
+    if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
+    d.straus_scratch = nullptr;
+    d.straus_cap = 0;
+    HIP_TRY(hipMalloc(&d.straus_scratch, lanes * stride));
+    d.straus_cap = lanes * stride;
   }
-  // the failing certificates' leaves: the list-mode leaf kernel's scratch and lists
+  // the failing sub-batches' leaves: the list-mode leaf kernel's scratch and lists
   const uint64_t lgrid = (uint64_t)d.cus * d.verify_blocks_per_cu;
   if (int rc = ensure_scratch(d, (size_t)lgrid * 256 * 2 * nwc::TAB_BYTES_PER_LANE, nvotes)) return rc;
   HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
   nwc::StrausArgs sa{};
-  sa.digests = dig; sa.voffs = voffs; sa.pks = pks; sa.sigs = sigs; sa.m = m; sa.lanes_per_cert = L;
+  sa.digests = dig; sa.msg_index = mi; sa.pks = pks; sa.sigs = sigs; sa.nv = nvotes; sa.runs = runs;
   {
     // 32 bytes from the host's CSPRNG per launch (dalek: merlin transcript + thread_rng)
     static thread_local std::random_device rd;
     for (int i = 0; i < 8; ++i) sa.seed[i] = rd();
   }
-  sa.comb16 = d.comb16; sa.scratch = d.straus_scratch; sa.lane_stride = stride; sa.cert_words = d.straus_cert;
-  HIP_TRY(hipMemsetAsync(d.straus_cert, 0, 8 * ((m + 63) / 64), s));
+  sa.comb16 = d.comb16; sa.scratch = d.straus_scratch; sa.lane_stride = stride;
+  sa.leaf_words = leaf; sa.list = d.uc_list; sa.count = d.uc_count;
+  HIP_TRY(hipMemsetAsync(leaf, 0, 8 * ((nvotes + 63) / 64), s));
   HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(nwc::k_verify_straus, dim3((unsigned)(lanes / 256)), dim3(256), 0, s, sa);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(nwc::k_straus_expand, dim3((unsigned)((nvotes + 255) / 256)), dim3(256), 0, s,
-                     (const uint64_t*)d.straus_cert, mi, nvotes, leaf, d.uc_list, d.uc_count);
   HIP_TRY(hipGetLastError());
   const nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
                           d.fb_count, 0u, nwc::Committee{}};

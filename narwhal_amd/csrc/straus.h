@@ -1,49 +1,61 @@
-// dalek's verify_batch equation, per certificate, as a Straus multi-scalar multiplication
-// (ed25519-dalek 1.0.1 batch.rs, called by crypto/src/lib.rs:206-219 Signature::verify_batch):
+// dalek's verify_batch equation (ed25519-dalek 1.0.1 batch.rs, called by
+// crypto/src/lib.rs:206-219 Signature::verify_batch) over sub-batches of votes, as a Straus
+// multi-scalar multiplication per lane:
 //
 //     sum_i z_i R_i + sum_i (z_i k_i mod l) A_i - (sum_i z_i s_i mod l) B == O
 //
-// with random 128-bit z_i.  One certificate is split over L consecutive lanes of a wave (L chosen
-// by the host, straus_lanes_per_cert, so that each lane holds at most STRAUS_MAX_PER_LANE votes
-// and the persistent grid's last round is nearly full); lane q takes
-// votes q, q + L, ... of its certificate and runs Straus over its 2 n_q points: the 63 x 4
-// doublings of its accumulator are shared by all of them, each window adds one entry per A_i
-// (signed radix-16 digits of z_i k_i mod l, 64 windows) and, in the low 33 windows, one per R_i
-// (digits of z_i).  The L partial sums meet through lane shuffles; lane 0 of the group adds
-// -(sum z_i s_i mod l) B from the radix-2^22 basepoint comb (12 entries, no doublings) and tests
-// the identity projectively.
+// with random 128-bit z_i.  The votes of a launch (any certificates; each vote reads its own
+// certificate digest) are cut into `runs` contiguous sub-batches of nq ~ 8-16 votes, one per lane
+// at a time (persistent grid).  A lane runs Straus over its 2 nq points: the 63 x 4 doublings of
+// its accumulator are shared by all of them, each window adds one entry per A_i (signed radix-16
+// digits of z_i k_i mod l, 64 windows) and, in the low 33 windows, one per R_i (digits of z_i);
+// then it adds -(sum z_i s_i mod l) B from the radix-2^22 basepoint comb (12 entries, no
+// doublings) and tests the identity projectively.  No lane talks to another: a sub-batch that
+// passes sets its votes' leaf bits, one that fails (a bad vote, an undecodable point, s >= l)
+// lists its votes for the exact per-vote leaf kernel.  So at a bad-vote rate f only ~1-(1-f)^nq
+// of the votes are verified twice, not every vote of a failing certificate.
 //
 // z_i = SHA-512(seed || u64le(global vote index))[..16], seed = 32 bytes the host draws per launch
 // from its CSPRNG (dalek draws z_i from a merlin transcript finalised with thread_rng: both are
 // 128-bit values the signers cannot predict).
 //
-// Semantics: a vote that does not parse or decode (s >= l, A or R not on
-// the curve) makes the certificate Err, as in dalek.  Otherwise this IS dalek's algorithm: Ok
-// when every e_i = s_i B - k_i A_i - R_i is O and every A_i torsion-free; Err w.p. 1 - 2^-128-ish
-// when some e_i has a prime-order component; and on dalek's randomized domain (pure-torsion
-// residuals, torsion-bearing keys) Ok w.p. ~1/ord, like dalek -- where the leaf kernels answer Err
-// deterministically.  A certificate that fails here is re-decided by the exact per-vote leaves
-// (the bad-vote set), so only passing certificates' verdicts come from this kernel.
+// Semantics: on the deterministic domain (every vote ok, or some vote with
+// a prime-order residual) the verdicts and the bad-vote set are exactly the leaves' (a sub-batch
+// holding an err vote passes w.p. ~2^-125, as dalek's batch).  On dalek's randomized domain
+// (pure-torsion residuals, torsion-bearing keys) a sub-batch passes w.p. ~1/ord, like dalek's
+// batch -- where the leaf kernels answer Err deterministically -- so this is a separate entry
+// point (nwc_dev_verify_batch_straus), not the default of nwc_verify_batch[_many].
 #pragma once
 
 namespace nwc {
 
-constexpr int STRAUS_MAX_PER_LANE = 24;
-// per vote in a lane's scratch: A's and R's 9-entry tables, then the digit strings
-constexpr size_t STRAUS_VOTE_BYTES = 2 * TAB_BYTES_PER_LANE + 64;
+#ifndef NWC_STRAUS_FULL_PREFETCH
+#define NWC_STRAUS_FULL_PREFETCH 1
+#endif
+#ifndef NWC_STRAUS_WAVES_PER_SIMD
+#define NWC_STRAUS_WAVES_PER_SIMD 2
+#endif
+constexpr int STRAUS_WAVES_PER_SIMD = NWC_STRAUS_WAVES_PER_SIMD;
+constexpr int STRAUS_MAX_PER_LANE = 16;
+// per vote in a lane's scratch: A's and R's 9-entry tables, then the digit strings (64 B), padded
+// to whole 128-B lines so every packed table entry of every vote is one cache line (an odd vote's
+// entries straddled two lines with a 64-B digit block: 23 KB fetched per vote instead of ~13)
+constexpr size_t STRAUS_VOTE_BYTES = (2 * TAB_BYTES_PER_LANE + 64 + 127) / 128 * 128;
 
 struct StrausArgs {
-  const uint8_t* digests;     // m x 32 (one per certificate)
-  const uint32_t* voffs;      // m + 1 vote offsets
+  const uint8_t* digests;     // certificate digests, 32 B each
+  const uint32_t* msg_index;  // per vote: its certificate (digest index)
   const uint8_t* pks;         // nv x 32
   const uint8_t* sigs;        // nv x 64
-  uint64_t m;
-  uint32_t lanes_per_cert;    // L: 1 .. 64
+  uint64_t nv;
+  uint64_t runs;              // sub-batch r = votes [r nv / runs, (r + 1) nv / runs), <= STRAUS_MAX_PER_LANE each
   uint32_t seed[8];
   const ge_niels_pad* comb16; // radix-2^22 basepoint comb
   uint8_t* scratch;           // lane_stride bytes per lane slot
-  uint64_t lane_stride;       // ceil(max votes / L) * STRAUS_VOTE_BYTES
-  uint64_t* cert_words;       // bit c = certificate c passed (zeroed by the caller)
+  uint64_t lane_stride;       // max votes per run * STRAUS_VOTE_BYTES
+  uint64_t* leaf_words;       // bit v = vote v's sub-batch passed (zeroed by the caller)
+  uint32_t* list;             // votes of the sub-batches that failed (for the exact leaves)
+  uint32_t* count;
 };
 
 // 128-bit z of global vote index v
@@ -106,41 +118,31 @@ __device__ __forceinline__ i32 nib_digit(const u32* words, int w) {
 // the ladder's digit reads then never wait on memory in front of their table gathers.
 constexpr int STRAUS_LDS_WORDS = 2 * STRAUS_MAX_PER_LANE * 256;
 
-__global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
+__global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_straus(StrausArgs a) {
   __shared__ u32 dl[STRAUS_LDS_WORDS];
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 L = a.lanes_per_cert;
-  // groups of L consecutive lanes inside a wave (64 / L groups; the last 64 mod L lanes idle)
-  const u32 lane = threadIdx.x & 63;
-  const u32 gpw = 64u / L;
-  const u32 gi = lane / L;
-  const u32 q = lane - gi * L;
-  const bool in_group = gi < gpw;
-  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  const uint64_t groups = waves * gpw;
+  const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
   uint8_t* const base = a.scratch + slot * a.lane_stride;
   // entry 0 (the identity) of the first vote's tables: the add every lane of a wave makes in a
   // (window, vote) step where it has no vote of its own reads it
   LaneTable{reinterpret_cast<uint4*>(base)}.store(0, ge_cached_identity());
   LaneTable{reinterpret_cast<uint4*>(base + TAB_BYTES_PER_LANE)}.store(0, ge_cached_identity());
-  // persistent: group g takes certificates g, g + groups, ...
-  for (uint64_t c0 = (slot >> 6) * gpw + gi; ; c0 += groups) {
+  // persistent: lane slot l takes sub-batches l, l + lanes, ...
+  for (uint64_t r0 = slot; ; r0 += lanes) {
     // wave-uniform loop exit: every lane of the wave leaves together
-    const bool active = in_group && c0 < a.m;
+    const bool active = r0 < a.runs;
     if (!__any(active)) break;
-    const uint64_t c = active ? c0 : 0;
-    const uint32_t o0 = active ? a.voffs[c] : 0, o1 = active ? a.voffs[c + 1] : 0;
-    const uint32_t nq = o1 > o0 + q ? (o1 - o0 - q + L - 1) / L : 0;
-    u32 mw[8];
-    load_words8(a.digests + 32 * c, mw);
+    const uint64_t v0 = active ? r0 * a.nv / a.runs : 0, v1 = active ? (r0 + 1) * a.nv / a.runs : 0;
+    const uint32_t nq = (uint32_t)(v1 - v0);
     bool ok = true;
     u32 S[8];
     _Pragma("unroll") for (int i = 0; i < 8; ++i) S[i] = 0;
     // ---- phase 1: per vote, decode, scalars, tables
 #pragma unroll 1
     for (uint32_t t = 0; t < nq; ++t) {
-      const uint64_t v = (uint64_t)o0 + q + (uint64_t)t * L;
-      u32 aw[8], sg[16];
+      const uint64_t v = v0 + t;
+      u32 mw[8], aw[8], sg[16];
+      load_words8(a.digests + 32 * (uint64_t)a.msg_index[v], mw);
       load_words8(a.pks + 32 * v, aw);
       load_words8(a.sigs + 64 * v, sg);
       load_words8(a.sigs + 64 * v + 32, sg + 8);
@@ -181,6 +183,7 @@ __global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
     // every lane of the wave runs the same window/vote schedule: the wave's largest nq
     uint32_t nw = nq;
     _Pragma("unroll") for (int msk = 32; msk >= 1; msk >>= 1) nw = max(nw, (uint32_t)__shfl_xor((int)nw, msk, 64));
+    nw = __builtin_amdgcn_readfirstlane(nw);
 #pragma unroll 1
     for (int w = 63; w >= 0; --w) {
       if ((w & 7) == 7) {
@@ -196,15 +199,33 @@ __global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
       if (w != 63) ladder_dbl4(t);
       const int sh = 4 * (w & 7);
       // the window's additions in order A_0, R_0, A_1, R_1, ... (R only in the low 33 windows):
-      // addition j = (vote j / per, kind j % per); each one's first gather is issued an addition ahead
-      const uint32_t per = w <= 32 ? 2u : 1u, nadd = nw * per;
+      // addition j = (vote j >> rs, kind j & rs); each one's first gather is issued an addition ahead
+      const uint32_t rs = w <= 32 ? 1u : 0u, nadd = nw << rs;
       auto entry = [&](uint32_t j, i32& d, LaneTable& tab) {
-        const uint32_t u = j / per, kind = j - u * per;
+        const uint32_t u = j >> rs, kind = j & rs;
         tab = LaneTable{reinterpret_cast<uint4*>(base + (size_t)(u < nq ? u : 0) * STRAUS_VOTE_BYTES +
                                                  kind * TAB_BYTES_PER_LANE)};
         d = (i32)((dl[(2 * u + kind) * 256 + threadIdx.x] >> sh) & 15u) - 8;
       };
 #if NWC_PACKED_TABLES
+#if NWC_STRAUS_FULL_PREFETCH
+      i32 dn;
+      LaneTable tn;
+      entry(0, dn, tn);
+      uint4 qn[8];
+      lt_load_full(tn, dn < 0 ? -dn : dn, dn < 0, qn);
+#pragma unroll 1
+      for (uint32_t j = 0; j < nadd; ++j) {
+        const bool neg = dn < 0;
+        uint4 cur[8];
+        _Pragma("unroll") for (int k = 0; k < 8; ++k) cur[k] = qn[k];
+        if (j + 1 < nadd) {
+          entry(j + 1, dn, tn);
+          lt_load_full(tn, dn < 0 ? -dn : dn, dn < 0, qn);
+        }
+        t = add_lt_full(t, cur, neg);
+      }
+#else
       i32 dn;
       LaneTable tn;
       entry(0, dn, tn);
@@ -221,6 +242,7 @@ __global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
         }
         t = add_lt_ab(t, cur, tab, d < 0 ? -d : d, d < 0);
       }
+#endif
 #else
 #pragma unroll 1
       for (uint32_t j = 0; j < nadd; ++j) {
@@ -231,26 +253,8 @@ __global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
       }
 #endif
     }
-    // ---- phase 3: the group's partial sums (a segmented tree towards q = 0), -S B, identity test
+    // ---- phase 3: + (-S) B from the basepoint comb, identity test
     ge_p3 P = ge_p1p1_to_p3(t);
-#pragma unroll 1
-    for (u32 off = 1; off < L; off <<= 1) {
-      ge_p3 Q;
-      {
-        const fe* sp = &P.X;
-        fe* dp = &Q.X;
-        _Pragma("unroll") for (int k = 0; k < 4; ++k)
-          _Pragma("unroll") for (int i = 0; i < 10; ++i) dp[k].v[i] = __shfl_down(sp[k].v[i], off, 64);
-      }
-      u32 So[8];
-      _Pragma("unroll") for (int i = 0; i < 8; ++i) So[i] = (u32)__shfl_down((int)S[i], off, 64);
-      const bool oko = __shfl_down((int)ok, off, 64) != 0;
-      if ((q & (2 * off - 1)) == 0 && q + off < L) {
-        P = ge_p1p1_to_p3(ge_add_cached(P, ge_p3_to_cached(Q)));
-        sc_add_l(S, So, S);
-        ok = ok && oko;
-      }
-    }
     // -S = l - S (S < l; S = 0 stays 0)
     u32 nS[8];
     {
@@ -272,51 +276,39 @@ __global__ __launch_bounds__(256, 2) void k_verify_straus(StrausArgs a) {
       P = ge_p1p1_to_p3(ge_add_niels(P, ge_niels_cneg(e, db < 0)));
     }
     const bool ident = fe_is_zero(P.X) && fe_is_zero(fe_sub(P.Y, P.Z));
-    if (active && q == 0 && ok && ident)
-      atomicOr(reinterpret_cast<unsigned long long*>(a.cert_words) + (c >> 6), 1ull << (c & 63));
+    if (active && nq) {
+      if (ok && ident) {
+        // the sub-batch's votes pass: set bits v0 .. v1-1 (at most two 64-bit words for nq <= 64)
+        for (uint64_t wv = v0 >> 6; wv <= (v1 - 1) >> 6; ++wv) {
+          const uint64_t lo = wv << 6;
+          const uint32_t b0 = v0 > lo ? (uint32_t)(v0 - lo) : 0u;
+          const uint32_t b1 = v1 - lo < 64 ? (uint32_t)(v1 - lo) : 64u;
+          const uint64_t m = (b1 - b0 == 64 ? ~0ull : ((1ull << (b1 - b0)) - 1ull)) << b0;
+          atomicOr(reinterpret_cast<unsigned long long*>(a.leaf_words) + wv, m);
+        }
+      } else {
+        const uint32_t at = atomicAdd(a.count, nq);
+        for (uint32_t q = 0; q < nq; ++q) a.list[at + q] = (uint32_t)(v0 + q);
+      }
+    }
   }
 }
 
-// Lanes per certificate for k_verify_straus: each lane pays ~252 doublings whatever it holds, and
-// a persistent grid of G groups gives each group ceil(m / G) certificates in turn, so the
-// last round can be nearly empty.  The host picks the L in 1..64 (any, not only powers of two)
-// that minimises (per-vote work + the doublings' share) / (round efficiency x lanes used), with
-// at most STRAUS_MAX_PER_LANE votes per lane.  Work in units of ~1k VALU instructions per vote.
-inline uint32_t straus_lanes_per_cert(uint64_t m, uint32_t maxv, uint64_t resident_waves) {
-  uint32_t best = 0;
-  double best_cost = 1e300;
-  for (uint32_t L = 1; L <= 64; ++L) {
-    const uint32_t nq = (maxv + L - 1) / L;
-    if (nq > (uint32_t)STRAUS_MAX_PER_LANE) continue;
-    const uint32_t gpw = 64 / L;
-    const double groups = (double)resident_waves * gpw;
-    const double rounds = (double)m / groups;
-    const double eff = (rounds / std::ceil(rounds)) * (double)(gpw * L) / 64.0;
-    const double cost = (230.0 + 245.0 / (double)(nq ? nq : 1)) / eff;
-    if (cost < best_cost) { best_cost = cost; best = L; }
-  }
-  return best;
-}
-
-// Largest certificate (votes) of a launch: one atomicMax per certificate (L is chosen from it).
-__global__ void k_cert_maxlen(const uint32_t* __restrict__ voffs, uint64_t m, uint32_t* __restrict__ out) {
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < m) atomicMax(out, voffs[c + 1] - voffs[c]);
-}
-
-// After k_verify_straus: a vote of a passing certificate gets its leaf bit set; a vote of a failing
-// one is listed for the exact leaf kernel (list mode ORs its verdict in), so that k_cert_reduce
-// gives the certificate verdicts and the exact bad-vote set.  One wave per 64 votes.
-__global__ void k_straus_expand(const uint64_t* __restrict__ cert_words, const uint32_t* __restrict__ msg_index,
-                                uint64_t nv, uint64_t* __restrict__ leaf_words, uint32_t* __restrict__ list,
-                                uint32_t* __restrict__ count) {
-  const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = v < nv;
-  const uint32_t c = in ? msg_index[v] : 0;
-  const bool pass = in && ((cert_words[c >> 6] >> (c & 63)) & 1);
-  const uint64_t bal = __ballot(pass);
-  if ((threadIdx.x & 63) == 0 && v < nv) leaf_words[v >> 6] = bal;
-  if (in && !pass) list[atomicAdd(count, 1u)] = (uint32_t)v;
+// Sub-batches of a launch of nv votes: each lane slot takes the same number of rounds, and the
+// runs are as close to `target` votes as that allows (never more than STRAUS_MAX_PER_LANE).  A
+// run costs ~253 doublings whatever it holds, so longer runs amortise them; a run with a bad vote
+// is verified again vote by vote, so shorter runs re-verify less at a given bad-vote rate
+// (target 12 by default, NWC_STRAUS_NQ to A/B).
+inline uint64_t straus_runs(uint64_t nv, uint64_t lanes, uint32_t target) {
+  if (target < 1) target = 1;
+  if (target > (uint32_t)STRAUS_MAX_PER_LANE) target = STRAUS_MAX_PER_LANE;
+  const uint64_t want = (nv + target - 1) / target;   // runs of <= target votes
+  if (want <= lanes) return want;
+  // every lane slot runs `rounds` sub-batches, of about `target` votes
+  uint64_t rounds = (want + lanes / 2) / lanes;
+  if (rounds < 1) rounds = 1;
+  while ((nv + rounds * lanes - 1) / (rounds * lanes) > (uint64_t)STRAUS_MAX_PER_LANE) ++rounds;
+  return rounds * lanes;
 }
 
 }  // namespace nwc

@@ -1,12 +1,13 @@
-"""dalek's batch equation per certificate on the GPU (k_verify_straus, nwc_dev_verify_batch_straus),
-leaves for the certificates it rejects: certificate verdicts and exact bad-vote sets against the
-golden batch fixtures and the oracle (crypto/src/lib.rs:206-219).
+"""dalek's batch equation over sub-batches of votes on the GPU (k_verify_straus,
+nwc_dev_verify_batch_straus), leaves for the sub-batches it rejects: certificate verdicts and exact
+bad-vote sets against the golden batch fixtures and the oracle (crypto/src/lib.rs:206-219).
 
 On the deterministic domain the outcome must be exact every run.  On dalek's randomized domain
 (fixture class "randomized": pure-torsion residuals, torsion-bearing keys) this path IS dalek's
 algorithm, so a certificate passes with probability ~1/ord and fails otherwise -- checked over
-repeated runs (fresh z_i each launch) as neither always-Ok nor always-Err; when it fails, the bad
-set is the leaves' (the fixture's)."""
+repeated runs (fresh z_i each launch) as neither always-Ok nor always-Err; when it fails, its bad
+set is a non-empty part of the leaves' (the fixture's): a randomized vote whose sub-batch passed
+is not in it."""
 import json
 import os
 
@@ -54,7 +55,10 @@ def test_golden_batches_straus(golden_batch):
             mine = sorted(int(v - offs[c]) for v in np.nonzero(bad[offs[c]:offs[c + 1]])[0] + offs[c])
             if b["class"] == "randomized":
                 passes[c] += int(cert[c])
-                assert mine == ([] if cert[c] else sorted(b["bad"])), b["name"]
+                if cert[c]:
+                    assert mine == [], b["name"]
+                else:
+                    assert mine and set(mine) <= set(b["bad"]), b["name"]
             else:
                 assert bool(cert[c]) == bool(b["verdict"]), b["name"]
                 assert mine == sorted(b["bad"]), b["name"]
@@ -66,9 +70,9 @@ def test_golden_batches_straus(golden_batch):
 
 @pytest.mark.parametrize("big", [383, 1600])
 def test_certificates_vs_oracle(oracle, big):
-    """Honest and 1 %-bad certificates of many sizes: with a 383-vote certificate every launch splits
-    certificates over L = 16 lanes; with a 1,600-vote one (past 64 lanes x 24 votes) the call takes
-    the exact leaves.  Verdicts and bad sets equal the oracle's."""
+    """Honest and 1 %-bad certificates of many sizes (empty, single-vote, and 383 / 1,600 votes: the
+    sub-batches cut across certificate boundaries everywhere).  Verdicts and bad sets equal the
+    oracle's, at the default sub-batch size and at 1 and 16 votes per sub-batch."""
     rng = np.random.default_rng(41)
     sizes = [0, 1, 2, 3, 24, 25, 48, 49, 67, 67, 67, 100, 200, big] + [int(x) for x in rng.integers(1, 90, 120)]
     m = len(sizes)
@@ -84,7 +88,15 @@ def test_certificates_vs_oracle(oracle, big):
     bad = rng.random(nv) < 0.01
     sigs[bad, 33] ^= 1
     ocert, obad = oracle.batch_many(dig, offs.astype(np.uint32), pks, sigs)
-    cert, gbad = _run(dig, offs, pks, sigs)
-    assert (cert == ocert).all(), np.nonzero(cert != ocert)
-    assert (gbad == obad).all()
+    for nq in (None, "1", "16"):
+        if nq is None:
+            os.environ.pop("NWC_STRAUS_NQ", None)
+        else:
+            os.environ["NWC_STRAUS_NQ"] = nq
+        try:
+            cert, gbad = _run(dig, offs, pks, sigs)
+        finally:
+            os.environ.pop("NWC_STRAUS_NQ", None)
+        assert (cert == ocert).all(), (nq, np.nonzero(cert != ocert))
+        assert (gbad == obad).all(), nq
     assert ocert.sum() > m // 3 and (~ocert).sum() > 3

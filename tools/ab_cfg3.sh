@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of library builds on the config-3 committee leg (100k certificates x 67 votes, cached keys:
-# k_verify_comb), interleaved for ROUNDS rounds.   tools/ab_cfg3.sh ROUNDS lib1.so lib2.so ...
+# A/B of library builds on the config-3 legs (100k certificates x 67 votes: leaves, Straus sub-batches,
+# clean, committee comb), interleaved for ROUNDS rounds.   tools/ab_cfg3.sh ROUNDS lib1.so lib2.so ...
 set -e
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 ROUNDS=$1; shift
@@ -12,7 +12,7 @@ for r in $(seq 1 $ROUNDS); do
     python3 -c "
 import json
 d=json.loads(open('$R/gpurun_out/ab3_last.json').read().strip().splitlines()[-1])['configs']['cfg3']
-print('%-34s cache %7.1f M votes/s ok=%s   no_cache %6.1f M votes/s ok=%s' % ('$lib', d['cache']['votes_per_s']/1e6, d['cache']['parity_ok'], d['no_cache']['votes_per_s']/1e6, d['no_cache']['parity_ok']))
+print('%-34s ' % '$lib' + '  '.join('%s %.1f%s' % (k, v['votes_per_s'] / 1e6, '' if v.get('parity_ok') else ' PARITY-FAIL') for k, v in d.items() if isinstance(v, dict) and 'votes_per_s' in v))
 " | tee -a $R/gpurun_out/ab3.txt
   done
 done
