@@ -25,6 +25,7 @@ struct Digester {
   uint32_t max_group, max_wait_us;
   int hip_id;
   unsigned copy_threads = 8;        // host threads filling a pinned stage (NWC_DIGEST_COPY_THREADS)
+  bool timing = false;              // NWC_DIGEST_TIMING: per-group fill / DMA-wait times on stderr
   std::mutex mu;
   std::condition_variable cv_in, cv_out;
   std::deque<Item> in;
@@ -110,9 +111,15 @@ struct Digester {
     int s = 0;
     bool used[2] = {false, false};
     size_t first = 0;   // first batch that may overlap the current stage
+    using clk = std::chrono::steady_clock;
+    double t_wait = 0, t_fill = 0;
+    const auto t_start = clk::now();
     for (uint64_t pos = 0; pos < total; pos += STAGE) {
       const uint64_t end = std::min<uint64_t>(pos + STAGE, total);
+      const auto t0 = clk::now();
       if (used[s]) HIP_TRY(hipEventSynchronize(stage_ev[s]));   // its previous DMA has landed
+      const auto t1 = clk::now();
+      t_wait += std::chrono::duration<double>(t1 - t0).count();
       while (first < k && hse[k + first] <= pos) ++first;   // batches wholly in earlier stages
       auto copy_range = [&](uint64_t lo, uint64_t hi) {
         // batches overlapping [lo, hi), found from `first` (starts are ascending)
@@ -135,6 +142,7 @@ struct Digester {
         copy_range(pos, std::min<uint64_t>(end, pos + per));
         for (auto& x : th) x.join();
       }
+      t_fill += std::chrono::duration<double>(clk::now() - t1).count();
       HIP_TRY(hipMemcpyAsync(ddata + pos, stage[s], bytes, hipMemcpyHostToDevice, stream));
       HIP_TRY(hipEventRecord(stage_ev[s], stream));
       used[s] = true;
@@ -145,6 +153,10 @@ struct Digester {
     HIP_TRY(hipMemcpyAsync(hout, dout, 32 * k, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     std::memcpy(out32, hout, 32 * k);
+    if (timing)
+      std::fprintf(stderr, "nwc digester: group %zu, %.1f MB: fill %.2f ms (%.1f GB/s), waits on DMA %.2f ms, total %.2f ms\n",
+                   k, total / 1e6, t_fill * 1e3, total / std::max(t_fill, 1e-9) / 1e9, t_wait * 1e3,
+                   std::chrono::duration<double>(clk::now() - t_start).count() * 1e3);
     return 0;
   }
 
@@ -204,6 +216,7 @@ nwc_digester* nwc_digester_create(uint32_t max_group, uint32_t max_wait_us) {
   q->max_wait_us = max_wait_us;
   q->hip_id = ctx(t_dev < (int)g_devs.size() ? t_dev : 0)->hip_id;
   if (const char* e = std::getenv("NWC_DIGEST_COPY_THREADS")) q->copy_threads = std::max(1, std::atoi(e));
+  q->timing = std::getenv("NWC_DIGEST_TIMING") != nullptr;
   if (q->init()) {
     q->release();
     delete q;

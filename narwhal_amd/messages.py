@@ -213,5 +213,6 @@ def sanitize_many(messages: Sequence[bytes], committee: Committee, gc_round: int
     _lib.check(lib.nwc_sanitize_messages(_lib.buf(data), offsets, m, gc_round, _lib.buf(target) if target else None,
                                          codes, dig, None))
     if digests is not None:
-        digests.extend(Digest(dig.raw[32 * i:32 * i + 32]) for i in range(m))
+        raw = dig.raw   # one copy (`.raw` copies the whole buffer on every access)
+        digests.extend(Digest(raw[32 * i:32 * i + 32]) for i in range(m))
     return [None if c == 0 else DagError(c) for c in codes]

@@ -66,7 +66,8 @@ class Digester:
         digs = ctypes.create_string_buffer(32 * max_n)
         n = ctypes.c_size_t(0)
         rc = self.lib.nwc_digester_poll(self.h, max_n, wait_us, tags, digs, ctypes.byref(n))
-        out = [(int(tags[i]), digs.raw[32 * i:32 * i + 32]) for i in range(n.value)]
+        raw = digs.raw[:32 * n.value]   # one copy: `.raw` copies the whole buffer on every access
+        out = [(int(tags[i]), raw[32 * i:32 * i + 32]) for i in range(n.value)]
         with self._lock:
             for t, _ in out:
                 self._held.pop(t, None)
