@@ -7,18 +7,74 @@
 // whatever else arrives within `max_wait_us` (up to `max_group` batches), and digests the group with
 // one launch.  Results come back in submission order.
 //
-// Data path per group: the borrowed batches are gathered into two pinned 64-MB stages in turn
-// (16-byte-aligned starts, the kernel's dwordx4 path; each stage filled by up to 8 host threads, as
-// one memcpy thread moves only ~10 GB/s) and DMA'd on the digester's own stream into one device
-// buffer while the next stage is filled; then k_sha512_digest32[_sched] over the group
+// Data path per group: the borrowed batches are gathered into NWC_DIGEST_STAGES (4) pinned 32-MB
+// stages in rotation (16-byte-aligned starts, the kernel's dwordx4 path; each stage filled by a
+// fixed pool of up to 8 host threads) and DMA'd on the digester's own stream into one device
+// buffer while the next stages are filled; then k_sha512_digest32[_sched] over the group
 // and one D2H of 32 bytes per batch.  The digester has its own stream and buffers (it does not
 // serialise with verification calls on the device's context).  Included by nwc_api.hip.
 #pragma once
 #include <array>
+#include <functional>
 #include <condition_variable>
 #include <deque>
 
 namespace {
+
+// A fixed set of host threads that fill one pinned stage together (each a contiguous byte range):
+// one memcpy thread moves ~30 GB/s, and spawning threads per 32-MB stage costs ~10 % of the fill.
+struct CopyPool {
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv, cv_done;
+  uint64_t gen = 0;
+  unsigned used = 0, pending = 0;
+  bool quit = false;
+  std::function<void(unsigned)> job;
+  void start(unsigned n) {   // n - 1 helpers; the caller is part 0
+    for (unsigned i = 1; i < n; ++i)
+      th.emplace_back([this, i] {
+        uint64_t seen = 0;
+        for (;;) {
+          std::unique_lock<std::mutex> lk(m);
+          cv.wait(lk, [&] { return quit || gen != seen; });
+          if (quit) return;
+          seen = gen;
+          if (i >= used) continue;
+          auto f = job;
+          lk.unlock();
+          f(i);
+          lk.lock();
+          if (--pending == 0) cv_done.notify_one();
+        }
+      });
+  }
+  // f(0 .. parts-1), part 0 on the calling thread
+  void run(unsigned parts, const std::function<void(unsigned)>& f) {
+    parts = std::min<unsigned>(parts, (unsigned)th.size() + 1);
+    if (parts <= 1) { f(0); return; }
+    {
+      std::lock_guard<std::mutex> lk(m);
+      job = f;
+      used = parts;
+      pending = parts - 1;
+      ++gen;
+    }
+    cv.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(m);
+    cv_done.wait(lk, [&] { return pending == 0; });
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      quit = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+    th.clear();
+  }
+};
 
 struct Digester {
   struct Item { const uint8_t* p; size_t len; uint64_t tag; };
@@ -36,11 +92,14 @@ struct Digester {
   bool stop = false;
   uint64_t groups = 0, batches = 0, bytes = 0;
   std::thread th;
+  CopyPool pool;
   // device side (touched by the drain thread only)
   hipStream_t stream = nullptr;
-  static constexpr size_t STAGE = 64u << 20;
-  uint8_t* stage[2] = {nullptr, nullptr};
-  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  static constexpr size_t STAGE = 32u << 20;
+  static constexpr int MAX_STAGES = 8;
+  int nstages = 4;                  // pinned stages in rotation (NWC_DIGEST_STAGES, 2..8)
+  uint8_t* stage[MAX_STAGES] = {};
+  hipEvent_t stage_ev[MAX_STAGES] = {};
   uint8_t* ddata = nullptr;
   size_t ddata_cap = 0;
   uint64_t* dse = nullptr;        // starts then ends
@@ -50,9 +109,10 @@ struct Digester {
   uint8_t* hout = nullptr;        // pinned digests
 
   int init() {
+    pool.start(copy_threads);
     HIP_TRY(hipSetDevice(hip_id));
     HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < nstages; ++s) {
       // non-coherent: ordinary cached host pages for the copy threads (the default, fine-grained
       // kind is uncached for CPU stores and caps the gather at a few GB/s); the DMA reads it
       HIP_TRY(hipHostMalloc(&stage[s], STAGE, hipHostMallocNonCoherent));
@@ -61,9 +121,10 @@ struct Digester {
     return 0;
   }
   void release() {
+    pool.stop();
     (void)hipSetDevice(hip_id);
     if (stream) (void)hipStreamSynchronize(stream);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < MAX_STAGES; ++s) {
       if (stage[s]) (void)hipHostFree(stage[s]);
       if (stage_ev[s]) (void)hipEventDestroy(stage_ev[s]);
     }
@@ -109,7 +170,7 @@ struct Digester {
     // contiguous byte range of the stage) while the other's DMA is in flight.  Stage s covers the
     // device layout's bytes [pos, pos + STAGE); batch i sits at hse[i] (16-byte aligned starts).
     int s = 0;
-    bool used[2] = {false, false};
+    bool used[MAX_STAGES] = {};
     size_t first = 0;   // first batch that may overlap the current stage
     using clk = std::chrono::steady_clock;
     double t_wait = 0, t_fill = 0;
@@ -131,22 +192,17 @@ struct Digester {
         }
       };
       const uint64_t bytes = end - pos;
-      const unsigned nt = (unsigned)std::min<uint64_t>(copy_threads, (bytes + (4u << 20) - 1) / (4u << 20));
-      if (nt <= 1) {
-        copy_range(pos, end);
-      } else {
-        std::vector<std::thread> th;
-        const uint64_t per = (bytes + nt - 1) / nt;
-        for (unsigned t = 1; t < nt; ++t)
-          th.emplace_back(copy_range, pos + t * per, std::min<uint64_t>(end, pos + (t + 1) * per));
-        copy_range(pos, std::min<uint64_t>(end, pos + per));
-        for (auto& x : th) x.join();
-      }
+      const unsigned nt = (unsigned)std::min<uint64_t>(copy_threads, (bytes + (2u << 20) - 1) / (2u << 20));
+      const uint64_t per = (bytes + nt - 1) / nt;
+      pool.run(nt, [&](unsigned t) {
+        const uint64_t lo = pos + t * per;
+        if (lo < end) copy_range(lo, std::min<uint64_t>(end, lo + per));
+      });
       t_fill += std::chrono::duration<double>(clk::now() - t1).count();
       HIP_TRY(hipMemcpyAsync(ddata + pos, stage[s], bytes, hipMemcpyHostToDevice, stream));
       HIP_TRY(hipEventRecord(stage_ev[s], stream));
       used[s] = true;
-      s ^= 1;
+      s = (s + 1) % nstages;
     }
     HIP_TRY(hipMemcpyAsync(dse, hse, 16 * k, hipMemcpyHostToDevice, stream));
     if (int rc = launch_digest(ddata, dse, dse + k, k, dout, stream)) return rc;
@@ -216,6 +272,7 @@ nwc_digester* nwc_digester_create(uint32_t max_group, uint32_t max_wait_us) {
   q->max_wait_us = max_wait_us;
   q->hip_id = ctx(t_dev < (int)g_devs.size() ? t_dev : 0)->hip_id;
   if (const char* e = std::getenv("NWC_DIGEST_COPY_THREADS")) q->copy_threads = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("NWC_DIGEST_STAGES")) q->nstages = std::min(Digester::MAX_STAGES, std::max(2, std::atoi(e)));
   q->timing = std::getenv("NWC_DIGEST_TIMING") != nullptr;
   if (q->init()) {
     q->release();
