@@ -32,6 +32,9 @@ namespace nwc {
 #ifndef NWC_STRAUS_FULL_PREFETCH
 #define NWC_STRAUS_FULL_PREFETCH 1
 #endif
+#ifndef NWC_STRAUS_PREFETCH2
+#define NWC_STRAUS_PREFETCH2 0
+#endif
 #ifndef NWC_STRAUS_WAVES_PER_SIMD
 #define NWC_STRAUS_WAVES_PER_SIMD 2
 #endif
@@ -208,7 +211,30 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
         d = (i32)((dl[(2 * u + kind) * 256 + threadIdx.x] >> sh) & 15u) - 8;
       };
 #if NWC_PACKED_TABLES
-#if NWC_STRAUS_FULL_PREFETCH
+#if NWC_STRAUS_FULL_PREFETCH && NWC_STRAUS_PREFETCH2
+      // two additions ahead: the entry an add consumes was gathered ~2.9k instructions earlier
+      i32 d0, d1 = 0;
+      LaneTable tq;
+      entry(0, d0, tq);
+      uint4 q0[8], q1[8];
+      lt_load_full(tq, d0 < 0 ? -d0 : d0, d0 < 0, q0);
+      if (nadd > 1) {
+        entry(1, d1, tq);
+        lt_load_full(tq, d1 < 0 ? -d1 : d1, d1 < 0, q1);
+      }
+#pragma unroll 1
+      for (uint32_t j = 0; j < nadd; ++j) {
+        const bool neg = d0 < 0;
+        uint4 cur[8];
+        _Pragma("unroll") for (int k = 0; k < 8; ++k) { cur[k] = q0[k]; q0[k] = q1[k]; }
+        d0 = d1;
+        if (j + 2 < nadd) {
+          entry(j + 2, d1, tq);
+          lt_load_full(tq, d1 < 0 ? -d1 : d1, d1 < 0, q1);
+        }
+        t = add_lt_full(t, cur, neg);
+      }
+#elif NWC_STRAUS_FULL_PREFETCH
       i32 dn;
       LaneTable tn;
       entry(0, dn, tn);

@@ -94,3 +94,32 @@ def test_processor_reference_batch():
         assert msgs[0] == struct.pack("<I", 0 if own else 1) + want + struct.pack("<I", 3)
         assert msgs[1:] == [worker_primary_message(_sha32(b), 3, own) for b in others]
         assert store[want] == batch and len(store) == len({_sha32(b) for b in [batch] + others})
+
+
+@pytest.mark.parametrize("stages,threads", [("2", "1"), ("4", "8"), ("8", "3")])
+def test_digester_stage_rotation(stages, threads):
+    """A 200-MB group through the pinned stages (32 MB each) in rotation: batches straddle stage
+    boundaries and every stage is refilled several times (NWC_DIGEST_STAGES / _COPY_THREADS are
+    read when the digester is created)."""
+    from narwhal_amd.processor import Digester
+    rng = np.random.default_rng(8)
+    base = rng.integers(0, 256, 600_000, dtype=np.uint8).tobytes()
+    lens = [int(x) for x in rng.integers(300_000, 600_000, 400)]
+    offs = [int(x) for x in rng.integers(0, 600_000 - 300_000, 400)]
+    batches = [base[o:o + n] for o, n in zip(offs, lens)]
+    os.environ["NWC_DIGEST_STAGES"], os.environ["NWC_DIGEST_COPY_THREADS"] = stages, threads
+    try:
+        dg = Digester(4096, 2_000_000)
+    finally:
+        del os.environ["NWC_DIGEST_STAGES"], os.environ["NWC_DIGEST_COPY_THREADS"]
+    try:
+        for b in batches:
+            dg.submit(b)
+        got = []
+        t0 = time.time()
+        while len(got) < len(batches) and time.time() - t0 < 60:
+            got += dg.poll(4096, 1_000_000)
+        assert [d for _, d in got] == [_sha32(b) for b in batches]
+        assert dg.stats()[0] == 1
+    finally:
+        dg.close()
