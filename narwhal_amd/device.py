@@ -50,8 +50,9 @@ def verify(msgs: torch.Tensor, pks: torch.Tensor, sigs: torch.Tensor, strict: bo
 
 def verify_batch_straus(digests: torch.Tensor, offsets: torch.Tensor, msg_index: torch.Tensor, pks: torch.Tensor,
                         sigs: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dalek's batch equation per certificate (Straus), the exact leaves for the certificates it
-    rejects: returns leaf-style verdict words (bit per vote) for cert_reduce.  Asynchronous."""
+    """dalek's batch equation over sub-batches of ~12 votes (Straus per lane), the exact leaves for
+    the sub-batches it rejects: returns leaf-style verdict words (bit per vote) for cert_reduce.
+    Asynchronous."""
     lib = _lib.load()
     m = offsets.numel() - 1
     n = pks.shape[0]

@@ -584,7 +584,7 @@ void orc_sign(const u8 seed[32], const u8 *msg, size_t mlen, u8 sig[64]) {
 
 /* ================================================================ multithreaded drivers */
 typedef struct {
-  int kind;  /* 0 strict, 1 leaf, 2 batch-certs, 3 digest */
+  int kind;  /* 0 strict, 1 leaf, 2 batch-certs, 3 digest, 4 batch-certs (Straus), 5 vote class + 1 */
   const u8 *msgs, *pks, *sigs; const u64 *offsets; const u32 *voffs; const u8 *data;
   u8 *out, *out2; size_t lo, hi;
 } job_t;
@@ -594,6 +594,7 @@ static void *worker(void *p) {
   for (size_t i = j->lo; i < j->hi; ++i) {
     if (j->kind == 0) j->out[i] = (u8)orc_verify_strict(j->msgs + 32 * i, j->pks + 32 * i, j->sigs + 64 * i);
     else if (j->kind == 1) j->out[i] = (u8)orc_leaf(j->msgs + 32 * i, j->pks + 32 * i, j->sigs + 64 * i);
+    else if (j->kind == 5) j->out[i] = (u8)(orc_vote_class(j->msgs + 32 * i, j->pks + 32 * i, j->sigs + 64 * i) + 1);
     else if (j->kind == 2) {
       u32 a = j->voffs[i], b = j->voffs[i + 1];
       j->out[i] = (u8)orc_verify_batch(j->msgs + 32 * i, j->pks + 32 * (size_t)a, j->sigs + 64 * (size_t)a, b - a,
@@ -633,6 +634,11 @@ void orc_verify_strict_many(const u8 *msgs, const u8 *pks, const u8 *sigs, size_
 }
 void orc_leaf_many(const u8 *msgs, const u8 *pks, const u8 *sigs, size_t n, u8 *out, int nthreads) {
   job_t j; memset(&j, 0, sizeof j); j.kind = 1; j.msgs = msgs; j.pks = pks; j.sigs = sigs; j.out = out;
+  run_jobs(j, n, nthreads);
+}
+/* orc_vote_class of n triples, stored + 1 (0 = parse/decode failure, 1 = ok, 2 = randomized, 3 = err) */
+void orc_vote_class_many(const u8 *msgs, const u8 *pks, const u8 *sigs, size_t n, u8 *out, int nthreads) {
+  job_t j; memset(&j, 0, sizeof j); j.kind = 5; j.msgs = msgs; j.pks = pks; j.sigs = sigs; j.out = out;
   run_jobs(j, n, nthreads);
 }
 /* m certificates: digests[32*m], vote ranges voffs[m+1] into pks/sigs; cert_ok[m], bad[votes] */

@@ -25,7 +25,7 @@ class Oracle:
         lib.orc_sha512.argtypes = [vp, sz, vp]
         lib.orc_public_key.argtypes = [vp, vp]
         lib.orc_sign.argtypes = [vp, vp, sz, vp]
-        for f in ("orc_verify_strict_many", "orc_leaf_many"):
+        for f in ("orc_verify_strict_many", "orc_leaf_many", "orc_vote_class_many"):
             getattr(lib, f).argtypes = [vp, vp, vp, sz, vp, ctypes.c_int]
         lib.orc_verify_batch_many.argtypes = [vp, vp, vp, vp, sz, vp, vp, ctypes.c_int]
         lib.orc_verify_batch_straus.argtypes = [vp, vp, vp, sz, ctypes.c_uint64]
@@ -73,6 +73,13 @@ class Oracle:
         out = np.zeros(n, dtype=np.uint8)
         self.lib.orc_leaf_many(self._p(msgs), self._p(pks), self._p(sigs), n, self._p(out), threads)
         return out.astype(bool)
+
+    def vote_class_many(self, msgs: np.ndarray, pks: np.ndarray, sigs: np.ndarray, threads: int = 8) -> np.ndarray:
+        """orc_vote_class per triple: -1 parse/decode failure, 0 ok, 1 randomized, 2 err."""
+        n = len(msgs)
+        out = np.empty(n, np.uint8)
+        self.lib.orc_vote_class_many(self._p(msgs), self._p(pks), self._p(sigs), n, self._p(out), threads)
+        return out.astype(np.int8) - 1
 
     def batch_many(self, digests: np.ndarray, offsets: np.ndarray, pks: np.ndarray, sigs: np.ndarray,
                    threads: int = 8):

@@ -4,10 +4,14 @@ has (bit flips in R / s / A / msg, s + l, small-order and non-canonical R and A 
 and A bytes, the golden edge cases tiled in), verified on the GPU in strict and batch-leaf mode
 and compared verdict by verdict with the CPU restatement (oracle/, multithreaded).
 
-    python tests/soak.py [--n 8388608] [--chunk 1048576] [--committee K] [--call C] [--out gpurun_out/soak.json]
+    python tests/soak.py [--n 8388608] [--chunk 1048576] [--committee K] [--call C] [--straus] [--out gpurun_out/soak.json]
 
 --call C verifies each chunk in device calls of at most C equations (C <= 1024 without a
 committee: the cold kernel, k_verify_cold, one block per equation).
+--straus also runs every chunk through dalek's batch equation over sub-batches
+(nwc_dev_verify_batch_straus, each triple its own certificate, so sub-batches mix every class):
+its per-vote bits must equal the oracle leaf on every vote outside dalek's randomized domain
+(orc_vote_class 1), where either outcome is dalek's.
 
 Test infrastructure (it runs the oracle), kept under tests/ like the oracle helpers; not part of
 the default pytest run (minutes of CPU oracle time).
@@ -42,9 +46,10 @@ CLASSES = ["valid", "flip_R", "flip_s", "flip_A", "flip_msg", "s_plus_l", "small
            "random_R", "random_A", "noncanon_R", "golden"]
 
 
-def mutate(rng, m, p, s, golden):
+def mutate(rng, m, p, s, golden, valid_frac=0.30):
     n = len(p)
-    kind = rng.choice(len(CLASSES), n, p=[0.30, 0.07, 0.07, 0.07, 0.07, 0.06, 0.06, 0.06, 0.06, 0.06, 0.06, 0.06])
+    rest = np.array([0.07, 0.07, 0.07, 0.07, 0.06, 0.06, 0.06, 0.06, 0.06, 0.06, 0.06])
+    kind = rng.choice(len(CLASSES), n, p=np.concatenate([[valid_frac], rest / rest.sum() * (1 - valid_frac)]))
     idx = lambda k: np.nonzero(kind == k)[0]  # noqa: E731
     i = idx(1); s[i, rng.integers(0, 32, len(i))] ^= (1 << rng.integers(0, 8, len(i))).astype(np.uint8)
     i = idx(2); s[i, 32 + rng.integers(0, 32, len(i))] ^= (1 << rng.integers(0, 8, len(i))).astype(np.uint8)
@@ -80,6 +85,9 @@ def main():
                     help="K > 0: signers drawn from K keys registered with nwc_set_committee (comb path, "
                          "cached ladder and the uncached list for mutated keys)")
     ap.add_argument("--call", type=int, default=0, help="C > 0: device calls of at most C equations")
+    ap.add_argument("--straus", action="store_true", help="also the Straus sub-batch path (per-vote bits vs the oracle)")
+    ap.add_argument("--valid-frac", type=float, default=0.30,
+                    help="share of unmutated triples (0.99: most Straus sub-batches pass, the rest exercise the leaves)")
     args = ap.parse_args()
     lib = _lib.load()
     if args.committee:
@@ -94,7 +102,8 @@ def main():
     cases = [c for c in gold["cases"] if len(c["msg"]) == 64]
     golden = tuple(np.stack([np.frombuffer(bytes.fromhex(c[k]), np.uint8) for c in cases]) for k in ("msg", "pk", "sig"))
     rng = np.random.default_rng(20261016)
-    stats = {c: {"n": 0, "strict_valid": 0, "leaf_valid": 0, "strict_mismatch": 0, "leaf_mismatch": 0} for c in CLASSES}
+    stats = {c: {"n": 0, "strict_valid": 0, "leaf_valid": 0, "strict_mismatch": 0, "leaf_mismatch": 0,
+                 "straus_mismatch": 0, "randomized": 0, "straus_randomized_pass": 0} for c in CLASSES}
     t0 = time.time()
     done = 0
     mism = []
@@ -109,7 +118,7 @@ def main():
         pks, sigs = device.keygen_sign(seeds, msgs)
         torch.cuda.synchronize()
         m, p, s = (t.cpu().numpy().copy() for t in (msgs, pks, sigs))
-        kind = mutate(rng, m, p, s, golden)
+        kind = mutate(rng, m, p, s, golden, args.valid_frac)
         tm, tp, ts = (torch.from_numpy(x).cuda() for x in (m, p, s))
         def run(strict):
             step = args.call or n
@@ -119,10 +128,20 @@ def main():
         gs, gl = run(True), run(False)
         os_ = orc.strict_many(m, p, s, threads=threads)
         ol = orc.leaf_many(m, p, s, threads=threads)
-        for j in np.nonzero((gs != os_) | (gl != ol))[0][:20]:
+        if args.straus:
+            ar = torch.arange(n + 1, dtype=torch.int32, device="cuda")
+            gb = device.unpack_bits(device.verify_batch_straus(tm, ar, ar[:n], tp, ts), n)
+            cls = orc.vote_class_many(m, p, s, threads=threads)
+            rnd = cls == 1
+            smis = (gb != ol) & ~rnd
+        else:
+            gb = np.zeros(n, bool)
+            rnd = smis = np.zeros(n, bool)
+        for j in np.nonzero((gs != os_) | (gl != ol) | smis)[0][:20]:
             mism.append({"class": CLASSES[kind[j]], "index": int(done + j), "msg": m[j].tobytes().hex(),
                          "pk": p[j].tobytes().hex(), "sig": s[j].tobytes().hex(), "gpu_strict": bool(gs[j]),
-                         "oracle_strict": bool(os_[j]), "gpu_leaf": bool(gl[j]), "oracle_leaf": bool(ol[j])})
+                         "oracle_strict": bool(os_[j]), "gpu_leaf": bool(gl[j]), "oracle_leaf": bool(ol[j]),
+                         "gpu_straus": bool(gb[j]) if args.straus else None})
         for k, name in enumerate(CLASSES):
             sel = kind == k
             st = stats[name]
@@ -131,15 +150,20 @@ def main():
             st["leaf_valid"] += int(ol[sel].sum())
             st["strict_mismatch"] += int((gs[sel] != os_[sel]).sum())
             st["leaf_mismatch"] += int((gl[sel] != ol[sel]).sum())
+            st["straus_mismatch"] += int(smis[sel].sum())
+            st["randomized"] += int(rnd[sel].sum())
+            st["straus_randomized_pass"] += int((rnd & (gb != 0))[sel].sum())
         done += n
         print("soak %d / %d  %.0f s" % (done, args.n, time.time() - t0), file=sys.stderr, flush=True)
-    total = {k: sum(v[k] for v in stats.values()) for k in ("n", "strict_mismatch", "leaf_mismatch")}
-    out = {"triples": args.n, "committee": args.committee, "call": args.call, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
+    total = {k: sum(v[k] for v in stats.values()) for k in ("n", "strict_mismatch", "leaf_mismatch", "straus_mismatch",
+                                                             "randomized", "straus_randomized_pass")}
+    out = {"triples": args.n, "committee": args.committee, "call": args.call, "straus": args.straus,
+           "valid_frac": args.valid_frac, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
            "mismatches": mism}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(out, open(args.out, "w"), indent=1)
     print(json.dumps(total))
-    return 0 if total["strict_mismatch"] == 0 and total["leaf_mismatch"] == 0 else 1
+    return 0 if total["strict_mismatch"] == 0 and total["leaf_mismatch"] == 0 and total["straus_mismatch"] == 0 else 1
 
 
 if __name__ == "__main__":

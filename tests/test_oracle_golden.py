@@ -156,6 +156,18 @@ def test_c_vote_class_matches_fixtures(oracle, golden_verify, golden_batch):
         assert exp == cls, name
 
 
+def test_c_vote_class_many_driver(oracle, golden_verify):
+    """The multithreaded vote-class driver (the Straus soak's checker) equals the per-vote class and
+    the leaf: class 0 exactly where the leaf holds."""
+    cs = [c for c in golden_verify["cases"] if len(c["msg"]) == 64]
+    m, p, s = (np.stack([np.frombuffer(bytes.fromhex(c[k]), np.uint8) for c in cs]) for k in ("msg", "pk", "sig"))
+    cls = oracle.vote_class_many(m, p, s, threads=3)
+    one = [oracle.lib.orc_vote_class(oracle._p(m[i]), oracle._p(p[i]), oracle._p(s[i])) for i in range(len(cs))]
+    assert cls.tolist() == one
+    assert ((cls == 0) == oracle.leaf_many(m, p, s).astype(bool)).all()
+    assert set(cls.tolist()) == {-1, 0, 1, 2}
+
+
 def test_straus_port_over_golden_cases(oracle, golden_verify, golden_batch):
     """The C port of dalek 1.0.1's verify_batch algorithm (random 128-bit z_i, (z_i hram_i mod l)
     on A_i, one Straus MSM; oracle/nwc_oracle.c orc_verify_batch_straus) run over 200 seeds on
