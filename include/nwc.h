@@ -93,9 +93,11 @@ int nwc_auto_cache_info(uint32_t* capacity, uint64_t* builds, uint64_t* hits);
  * max_wait_us (up to max_group batches), and digests the group with one GPU launch on its own
  * stream.  Batches are BORROWED: the caller keeps each one alive until its digest has been
  * polled (the Processor stores the batch after hashing it anyway).  Digests come back in
- * submission order with the caller's tag.  One 500-KB batch alone takes ~30 ms on the GPU (a
- * sequential SHA-512 chain on one lane) against ~0.36 ms on one host core: the GPU pays only for
- * groups of ~1,000+ batches.  create returns NULL on failure
+ * submission order with the caller's tag.  One 500-KB batch alone takes ~28 ms on the GPU (a
+ * sequential SHA-512 chain on one lane) against ~0.36 ms on one host core: measured, the GPU ties 16
+ * host cores at ~1,000 batches per group and is ~2.3x faster at 100,000 (PCIe-bound, ~36 GB/s;
+ * INTEGRATION.md §4).  Data path: NWC_DIGEST_STAGES (4) pinned 32-MB stages filled by
+ * NWC_DIGEST_COPY_THREADS (8) host threads.  create returns NULL on failure
  * (nwc_last_error); poll waits up to wait_us for at least one digest and reports a device error
  * of the drain thread (sticky); destroy digests what is queued, then frees the digester. */
 typedef struct nwc_digester nwc_digester;
