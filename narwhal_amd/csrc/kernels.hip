@@ -802,11 +802,17 @@ typedef __attribute__((address_space(3))) void nwc_lvoid;
 #ifndef NWC_LADDER_PREFETCH
 #define NWC_LADDER_PREFETCH 0
 #endif
+// cache policy of the basepoint-entry DMA (random rows of the 2.1 GB tables, used once): 0 =
+// default, 2 = non-temporal (A/B: keep L2/MALL for the per-lane tables)
+#ifndef NWC_BASE_FETCH_CPOL
+#define NWC_BASE_FETCH_CPOL 0
+#endif
 constexpr int STAGE_U4_PER_WAVE = NWC_STAGE_ENTRIES * 8 * 64;
 __device__ __forceinline__ void stage_fetch(uint4* stage, int e, const ge_niels_pad* src) {
   const uint4* g = reinterpret_cast<const uint4*>(src);
   _Pragma("unroll") for (int c = 0; c < 8; ++c)
-    __builtin_amdgcn_global_load_lds((nwc_gvoid*)(g + c), (nwc_lvoid*)(stage + (8 * e + c) * 64), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((nwc_gvoid*)(g + c), (nwc_lvoid*)(stage + (8 * e + c) * 64), 16, 0,
+                                     NWC_BASE_FETCH_CPOL);
 }
 __device__ __forceinline__ ge_niels stage_read(const uint4* stage, int e) {
   const int lane = threadIdx.x & 63;
