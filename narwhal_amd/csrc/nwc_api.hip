@@ -613,6 +613,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
                   hipStream_t s, int flags = 0, uint8_t* vbytes = nullptr) {
   if (n == 0) return 0;
+  // equation indices travel as uint32 (fallback / uncached / torsion lists)
+  if (n > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "more than 2^32 - 1 equations in one launch");
   const VPath path = verify_path();
   if ((flags & LV_AUTO) && (flags & LV_ALL_CACHED) && path == VPath::Default && n <= NWC_WIDE_MAX && d.ak_n) {
     // latency path over the auto key cache (same kernel, the auto cache as its committee)
@@ -1374,6 +1376,7 @@ int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, co
   const auto* pks = static_cast<const uint8_t*>(d_pks);
   const auto* sigs = static_cast<const uint8_t*>(d_sigs);
   auto* leaf = static_cast<uint64_t*>(d_leaf_words);
+  if (nvotes > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "more than 2^32 - 1 votes in one call");
   if (!d.comb16)   // no basepoint comb (NWC_COMB16=0): the exact leaves
     return launch_verify(d, dig, mi, 0, pks, sigs, nvotes, 0, leaf, s);
   (void)voffs;
