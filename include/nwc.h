@@ -162,7 +162,8 @@ int nwc_sha512_trunc32_many(const uint8_t* data, const uint64_t* offsets, size_t
 
 /* ---- device-resident variants (inputs already in HBM) ---------------------------------- */
 /* strict != 0: verify_strict semantics; strict == 0: batch-leaf semantics.  msg_index
- * (nullable, device u32[n]) selects the digest of equation i; otherwise digest i*msg_stride. */
+ * (nullable, device u32[n]) selects the digest of equation i; otherwise digest i*msg_stride.
+ * n < 2^32 per call (NWC_ERR_ARG otherwise). */
 int nwc_dev_verify(const void* d_msgs, const void* d_msg_index, uint64_t msg_stride,
                    const void* d_pks, const void* d_sigs, uint64_t n, int strict,
                    void* d_verdict_words, void* stream);
