@@ -10,12 +10,14 @@ set is a non-empty part of the leaves' (the fixture's): a randomized vote whose 
 is not in it."""
 import json
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
 import torch
 
-from tests.conftest import GOLDEN
+from tests.conftest import GOLDEN, ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -100,3 +102,12 @@ def test_certificates_vs_oracle(oracle, big):
         assert (cert == ocert).all(), (nq, np.nonzero(cert != ocert))
         assert (gbad == obad).all(), nq
     assert ocert.sum() > m // 3 and (~ocert).sum() > 3
+
+
+def test_without_basepoint_comb_takes_the_leaves():
+    """NWC_COMB16=0 (no radix-2^22 basepoint comb for the -S B term): the entry runs the exact leaves
+    instead; the oracle certificates must still match (a process of its own: the switch is read once)."""
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", "test_gpu_straus.py") + "::test_certificates_vs_oracle[383]"],
+                       env=dict(os.environ, NWC_COMB16="0"), cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
