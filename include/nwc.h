@@ -68,6 +68,15 @@ int nwc_verify_strict_many(const uint8_t* msgs32, const uint8_t* pks, const uint
 int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
                           const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap,
                           uint8_t* bad_vote_bitmap);
+/* The same m certificates through dalek's own batch equation (ed25519-dalek 1.0.1 batch.rs, the
+ * algorithm behind crypto/src/lib.rs:218): random 128-bit z_i, one Straus pass per sub-batch of
+ * ~12 votes on the GPU (nwc_dev_verify_batch_straus), the exact per-vote leaves for the sub-batches
+ * it rejects.  Same verdicts and bad sets as nwc_verify_batch_many on the deterministic domain; on
+ * dalek's randomized domain (pure-torsion residuals, torsion-bearing keys) dalek's probabilities
+ * instead of Err.  Faster on clean traffic, slower at ~1 % bad votes. */
+int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
+                                 const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap,
+                                 uint8_t* bad_vote_bitmap);
 
 /* Committee key cache (config/src/lib.rs:154-156 Committee).  Optional: verdicts never
  * depend on it. */

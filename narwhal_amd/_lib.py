@@ -34,6 +34,7 @@ _SIGS = {
     "nwc_verify_batch": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p]),
     "nwc_verify_strict_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p]),
     "nwc_verify_batch_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p, _c_u8p]),
+    "nwc_verify_batch_straus_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p, _c_u8p]),
     "nwc_set_committee": (ctypes.c_int, [_c_u8p, ctypes.c_size_t]),
     "nwc_cache_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_auto_cache_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

@@ -978,6 +978,113 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
   return 0;
 }
 
+// dalek's batch equation over sub-batches (k_verify_straus) + the exact leaves for the failing
+// sub-batches, on d's stream s: leaf words (a bit per vote) for cert_reduce.  Caller holds d.mu
+// and has set the device.
+int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8_t* pks, const uint8_t* sigs,
+                  uint64_t nvotes, uint64_t* leaf, hipStream_t s) {
+  if (nvotes == 0) return 0;
+  if (nvotes > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "more than 2^32 - 1 votes in one call");
+  if (!d.comb16)   // no basepoint comb (NWC_COMB16=0): the exact leaves
+    return launch_verify(d, dig, mi, 0, pks, sigs, nvotes, 0, leaf, s);
+  // sub-batches of ~NWC_STRAUS_NQ votes (default 12), every lane slot the same number of rounds
+  uint32_t target = 12;
+  if (const char* e = std::getenv("NWC_STRAUS_NQ")) target = (uint32_t)std::strtoul(e, nullptr, 10);   // A/B
+  const uint64_t resident = (uint64_t)d.cus * nwc::STRAUS_WAVES_PER_SIMD * 256;
+  const uint64_t runs = nwc::straus_runs(nvotes, resident, target);
+  const uint64_t lanes = std::min<uint64_t>((runs + 255) / 256 * 256, resident);
+  const uint64_t maxq = (nvotes + runs - 1) / runs;
+  const uint64_t stride = maxq * nwc::STRAUS_VOTE_BYTES;
+  if (lanes * stride > d.straus_cap) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
+    d.straus_scratch = nullptr;
+    d.straus_cap = 0;
+    HIP_TRY(hipMalloc(&d.straus_scratch, lanes * stride));
+    d.straus_cap = lanes * stride;
+  }
+  // the failing sub-batches' leaves: the list-mode leaf kernel's scratch and lists
+  const uint64_t lgrid = (uint64_t)d.cus * d.verify_blocks_per_cu;
+  if (int rc = ensure_scratch(d, (size_t)lgrid * 256 * 2 * nwc::TAB_BYTES_PER_LANE, nvotes)) return rc;
+  HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
+  nwc::StrausArgs sa{};
+  sa.digests = dig; sa.msg_index = mi; sa.pks = pks; sa.sigs = sigs; sa.nv = nvotes; sa.runs = runs;
+  {
+    // 32 bytes from the host's CSPRNG per launch (dalek: merlin transcript + thread_rng)
+    static thread_local std::random_device rd;
+    for (int i = 0; i < 8; ++i) sa.seed[i] = rd();
+  }
+  sa.comb16 = d.comb16; sa.scratch = d.straus_scratch; sa.lane_stride = stride;
+  sa.leaf_words = leaf; sa.list = d.uc_list; sa.count = d.uc_count;
+  HIP_TRY(hipMemsetAsync(leaf, 0, 8 * ((nvotes + 63) / 64), s));
+  HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(nwc::k_verify_straus, dim3((unsigned)(lanes / 256)), dim3(256), 0, s, sa);
+  HIP_TRY(hipGetLastError());
+  const nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
+                          d.fb_count, 0u, nwc::Committee{}};
+  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
+  hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3((unsigned)lgrid), dim3(256), 0, s, a, ca);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(16), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  if (int rc = launch_torsion(d, pks, leaf, nvotes, d.uc_list, d.uc_count, nwc::Committee{}, s)) return rc;
+  HIP_TRY(hipEventRecord(d.scratch_free, s));
+  return 0;
+}
+
+
+// Per-vote leaf bits of every device's share (whole certificates) -> certificate verdicts and the
+// bad-vote bitmap (a certificate passes iff every vote's bit is set; an empty one passes).
+int batch_verdicts(const uint32_t* offsets, size_t m, const std::vector<uint64_t>& cuts,
+                   const std::vector<std::vector<uint64_t>>& parts, uint8_t* cert_ok_bitmap, uint8_t* bad_vote_bitmap) {
+  const uint64_t nv = offsets[m];
+  std::vector<uint8_t> leafbytes((nv + 7) / 8 + 8, 0);
+  for (size_t i = 0; i + 1 < cuts.size(); ++i) merge_bits(leafbytes.data(), cuts[i], parts[i], cuts[i + 1] - cuts[i]);
+  std::memset(cert_ok_bitmap, 0, (m + 7) / 8);
+  for (size_t c = 0; c < m; ++c) {
+    bool ok = true;
+    for (uint32_t v = offsets[c]; v < offsets[c + 1]; ++v) ok = ok && ((leafbytes[v >> 3] >> (v & 7)) & 1);
+    if (ok) cert_ok_bitmap[c >> 3] |= (uint8_t)(1u << (c & 7));
+  }
+  if (bad_vote_bitmap) {
+    for (uint64_t v = 0; v < nv; ++v) {
+      const bool bad = !((leafbytes[v >> 3] >> (v & 7)) & 1);
+      bad_vote_bitmap[v >> 3] = (uint8_t)((bad_vote_bitmap[v >> 3] & ~(1u << (v & 7))) | ((unsigned)bad << (v & 7)));
+    }
+  }
+  return 0;
+}
+
+// One device's share of nwc_verify_batch_straus_many: votes [lo, hi) (whole certificates) staged
+// into the arena with one H2D each, the Straus launch, one D2H of the leaf words.
+int straus_range(int di, const uint8_t* digests, size_t m, const uint32_t* msg_index, const uint8_t* pks,
+                 const uint8_t* sigs, uint64_t lo, uint64_t hi, std::vector<uint64_t>& out_words) {
+  DevCtx& d = *ctx(di);
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  const uint64_t n = hi - lo;
+  const uint64_t words = (n + 63) / 64;
+  out_words.assign(words, 0);
+  if (n == 0) return 0;
+  const size_t need = align256(32 * m) + align256(4 * n) + align256(32 * n) + align256(64 * n) + align256(8 * words);
+  if (int rc = d.ensure_arena(need)) return rc;
+  Carve c(d.arena);
+  uint8_t* dm = c.take<uint8_t>(32 * m);
+  uint32_t* dmi = c.take<uint32_t>(4 * n);
+  uint8_t* dp = c.take<uint8_t>(32 * n);
+  uint8_t* ds = c.take<uint8_t>(64 * n);
+  uint64_t* dout = c.take<uint64_t>(8 * words);
+  HIP_TRY(hipMemcpyAsync(dm, digests, 32 * m, hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(hipMemcpyAsync(dmi, msg_index + lo, 4 * n, hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(hipMemcpyAsync(dp, pks + 32 * lo, 32 * n, hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(hipMemcpyAsync(ds, sigs + 64 * lo, 64 * n, hipMemcpyHostToDevice, d.stream));
+  if (int rc = launch_straus(d, dm, dmi, dp, ds, n, dout, d.stream)) return rc;
+  HIP_TRY(hipMemcpyAsync(out_words.data(), dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1166,21 +1273,33 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
   }
   for (auto& t : th) t.join();
   for (int r : rc) if (r < 0) return r;
-  std::vector<uint8_t> leafbytes((nv + 7) / 8 + 8, 0);
-  for (int i = 0; i < nd; ++i) merge_bits(leafbytes.data(), cuts[i], parts[i], cuts[i + 1] - cuts[i]);
-  std::memset(cert_ok_bitmap, 0, (m + 7) / 8);
-  for (size_t c = 0; c < m; ++c) {
-    bool ok = true;
-    for (uint32_t v = offsets[c]; v < offsets[c + 1]; ++v) ok = ok && ((leafbytes[v >> 3] >> (v & 7)) & 1);
-    if (ok) cert_ok_bitmap[c >> 3] |= (uint8_t)(1u << (c & 7));
-  }
-  if (bad_vote_bitmap) {
-    for (uint64_t v = 0; v < nv; ++v) {
-      const bool bad = !((leafbytes[v >> 3] >> (v & 7)) & 1);
-      bad_vote_bitmap[v >> 3] = (uint8_t)((bad_vote_bitmap[v >> 3] & ~(1u << (v & 7))) | ((unsigned)bad << (v & 7)));
-    }
-  }
-  return 0;
+  return batch_verdicts(offsets, m, cuts, parts, cert_ok_bitmap, bad_vote_bitmap);
+}
+
+int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
+                                 const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap, uint8_t* bad_vote_bitmap) {
+  if (int rc = require_init()) return rc;
+  if (m == 0) return 0;
+  if (!digests || !offsets || !cert_ok_bitmap) return set_err(NWC_ERR_ARG, "null buffer");
+  if (offsets[0] != 0) return set_err(NWC_ERR_ARG, "offsets[0] must be 0");
+  for (size_t c = 0; c < m; ++c)
+    if (offsets[c + 1] < offsets[c]) return set_err(NWC_ERR_ARG, "offsets not monotone at %zu", c);
+  const uint64_t nv = offsets[m];
+  if (nv && (!pks || !sigs)) return set_err(NWC_ERR_ARG, "null vote buffer");
+  std::vector<uint32_t> mi(nv);
+  for (size_t c = 0; c < m; ++c)
+    for (uint32_t v = offsets[c]; v < offsets[c + 1]; ++v) mi[v] = (uint32_t)c;
+  const int nd = (int)g_devs.size();
+  std::vector<uint64_t> cuts(nd + 1);
+  nwc_cert_cuts(offsets, m, (uint32_t)nd, cuts.data());
+  std::vector<int> rc(nd, 0);
+  std::vector<std::vector<uint64_t>> parts(nd);
+  std::vector<std::thread> th;
+  for (int i = 0; i < nd; ++i)
+    th.emplace_back([&, i] { rc[i] = straus_range(i, digests, m, mi.data(), pks, sigs, cuts[i], cuts[i + 1], parts[i]); });
+  for (auto& t : th) t.join();
+  for (int r : rc) if (r < 0) return r;
+  return batch_verdicts(offsets, m, cuts, parts, cert_ok_bitmap, bad_vote_bitmap);
 }
 
 // Committee updates are serialised: the devices' caches and the host's view of them (g_hcm, which
@@ -1370,60 +1489,9 @@ int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, co
   if (m == 0 || nvotes == 0) return 0;
   if (!d_digests || !d_offsets || !d_msg_index || !d_pks || !d_sigs || !d_leaf_words)
     return set_err(NWC_ERR_ARG, "null buffer");
-  const auto* dig = static_cast<const uint8_t*>(d_digests);
-  const auto* voffs = static_cast<const uint32_t*>(d_offsets);
-  const auto* mi = static_cast<const uint32_t*>(d_msg_index);
-  const auto* pks = static_cast<const uint8_t*>(d_pks);
-  const auto* sigs = static_cast<const uint8_t*>(d_sigs);
-  auto* leaf = static_cast<uint64_t*>(d_leaf_words);
-  if (nvotes > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "more than 2^32 - 1 votes in one call");
-  if (!d.comb16)   // no basepoint comb (NWC_COMB16=0): the exact leaves
-    return launch_verify(d, dig, mi, 0, pks, sigs, nvotes, 0, leaf, s);
-  (void)voffs;
-  // sub-batches of ~NWC_STRAUS_NQ votes (default 12), every lane slot the same number of rounds
-  uint32_t target = 12;
-  if (const char* e = std::getenv("NWC_STRAUS_NQ")) target = (uint32_t)std::strtoul(e, nullptr, 10);   // A/B
-  const uint64_t resident = (uint64_t)d.cus * nwc::STRAUS_WAVES_PER_SIMD * 256;
-  const uint64_t runs = nwc::straus_runs(nvotes, resident, target);
-  const uint64_t lanes = std::min<uint64_t>((runs + 255) / 256 * 256, resident);
-  const uint64_t maxq = (nvotes + runs - 1) / runs;
-  const uint64_t stride = maxq * nwc::STRAUS_VOTE_BYTES;
-  if (lanes * stride > d.straus_cap) {
-    HIP_TRY(hipStreamSynchronize(s));
-    if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
-    d.straus_scratch = nullptr;
-    d.straus_cap = 0;
-    HIP_TRY(hipMalloc(&d.straus_scratch, lanes * stride));
-    d.straus_cap = lanes * stride;
-  }
-  // the failing sub-batches' leaves: the list-mode leaf kernel's scratch and lists
-  const uint64_t lgrid = (uint64_t)d.cus * d.verify_blocks_per_cu;
-  if (int rc = ensure_scratch(d, (size_t)lgrid * 256 * 2 * nwc::TAB_BYTES_PER_LANE, nvotes)) return rc;
-  HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
-  nwc::StrausArgs sa{};
-  sa.digests = dig; sa.msg_index = mi; sa.pks = pks; sa.sigs = sigs; sa.nv = nvotes; sa.runs = runs;
-  {
-    // 32 bytes from the host's CSPRNG per launch (dalek: merlin transcript + thread_rng)
-    static thread_local std::random_device rd;
-    for (int i = 0; i < 8; ++i) sa.seed[i] = rd();
-  }
-  sa.comb16 = d.comb16; sa.scratch = d.straus_scratch; sa.lane_stride = stride;
-  sa.leaf_words = leaf; sa.list = d.uc_list; sa.count = d.uc_count;
-  HIP_TRY(hipMemsetAsync(leaf, 0, 8 * ((nvotes + 63) / 64), s));
-  HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
-  HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
-  hipLaunchKernelGGL(nwc::k_verify_straus, dim3((unsigned)(lanes / 256)), dim3(256), 0, s, sa);
-  HIP_TRY(hipGetLastError());
-  const nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
-                          d.fb_count, 0u, nwc::Committee{}};
-  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
-  hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3((unsigned)lgrid), dim3(256), 0, s, a, ca);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(16), dim3(256), 0, s, a);
-  HIP_TRY(hipGetLastError());
-  if (int rc = launch_torsion(d, pks, leaf, nvotes, d.uc_list, d.uc_count, nwc::Committee{}, s)) return rc;
-  HIP_TRY(hipEventRecord(d.scratch_free, s));
-  return 0;
+  return launch_straus(d, static_cast<const uint8_t*>(d_digests), static_cast<const uint32_t*>(d_msg_index),
+                       static_cast<const uint8_t*>(d_pks), static_cast<const uint8_t*>(d_sigs), nvotes,
+                       static_cast<uint64_t*>(d_leaf_words), s);
 }
 
 int nwc_dev_sha512_trunc32(const void* d_data, const void* d_offsets, uint64_t n, void* d_out32, void* stream) {

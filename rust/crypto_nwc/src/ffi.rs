@@ -21,6 +21,8 @@ extern "C" {
                                   verdict_bitmap: *mut u8) -> c_int;
     pub fn nwc_verify_batch_many(digests: *const u8, offsets: *const u32, pks: *const u8, sigs: *const u8, m: usize,
                                  cert_ok_bitmap: *mut u8, bad_vote_bitmap: *mut u8) -> c_int;
+    pub fn nwc_verify_batch_straus_many(digests: *const u8, offsets: *const u32, pks: *const u8, sigs: *const u8,
+                                        m: usize, cert_ok_bitmap: *mut u8, bad_vote_bitmap: *mut u8) -> c_int;
     pub fn nwc_set_committee(pks: *const u8, n: usize) -> c_int;
     pub fn nwc_cache_stats(committee_keys: *mut u32, auto_keys: *mut u32) -> c_int;
     pub fn nwc_auto_cache_info(capacity: *mut u32, builds: *mut u64, hits: *mut u64) -> c_int;

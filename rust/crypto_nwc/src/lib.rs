@@ -68,6 +68,29 @@ pub fn verify_batch(digest: &[u8; 32], public_keys: &[[u8; 32]], signatures: &[[
     })
 }
 
+/// Many certificates at once (certificate c = `digests[c]` over votes `offsets[c]..offsets[c+1]`):
+/// per-certificate verdicts and the bad-vote set.  `dalek_batch = false`: the exact per-vote leaves
+/// (deterministic; Err on dalek's randomized domain); `true`: dalek's own random-linear-combination
+/// equation over sub-batches, the leaves only where it fails (faster on clean traffic; dalek's
+/// probabilities on the randomized domain).  Returns (certificate ok, vote bad) as bitmaps.
+pub fn verify_batch_many(digests: &[[u8; 32]], offsets: &[u32], public_keys: &[[u8; 32]], signatures: &[[u8; 64]],
+                         dalek_batch: bool) -> (Vec<u8>, Vec<u8>) {
+    let m = digests.len();
+    assert_eq!(offsets.len(), m + 1);
+    assert_eq!(public_keys.len(), signatures.len());
+    assert_eq!(offsets[m] as usize, public_keys.len());
+    init(0);
+    let dg: Vec<u8> = digests.iter().flat_map(|d| d.iter().copied()).collect();
+    let pks: Vec<u8> = public_keys.iter().flat_map(|k| k.iter().copied()).collect();
+    let sigs: Vec<u8> = signatures.iter().flat_map(|s| s.iter().copied()).collect();
+    let mut ok = vec![0u8; (m + 7) / 8];
+    let mut bad = vec![0u8; (public_keys.len() + 7) / 8];
+    let f = if dalek_batch { ffi::nwc_verify_batch_straus_many } else { ffi::nwc_verify_batch_many };
+    let rc = unsafe { f(dg.as_ptr(), offsets.as_ptr(), pks.as_ptr(), sigs.as_ptr(), m, ok.as_mut_ptr(), bad.as_mut_ptr()) };
+    assert!(rc == 0, "libnwc failure {}", rc);
+    (ok, bad)
+}
+
 /// `Sha512::digest(bytes)[..32]` (worker/src/processor.rs:38).
 pub fn digest32(data: &[u8]) -> [u8; 32] {
     init(0);

@@ -25,6 +25,11 @@ bad = ctypes.create_string_buffer((int(offs[-1]) + 7) // 8)
 _lib.check(lib.nwc_verify_batch_many(_lib.buf(dig), _lib.buf(offs), _lib.buf(p), _lib.buf(s), mc, cert, bad))
 out["cert"] = np.frombuffer(cert.raw, np.uint8).copy()
 out["bad"] = np.frombuffer(bad.raw, np.uint8).copy()
+cert2 = ctypes.create_string_buffer((mc + 7) // 8)
+bad2 = ctypes.create_string_buffer((int(offs[-1]) + 7) // 8)
+_lib.check(lib.nwc_verify_batch_straus_many(_lib.buf(dig), _lib.buf(offs), _lib.buf(p), _lib.buf(s), mc, cert2, bad2))
+out["cert_straus"] = np.frombuffer(cert2.raw, np.uint8).copy()
+out["bad_straus"] = np.frombuffer(bad2.raw, np.uint8).copy()
 blob, boffs = d["blob"], d["boffs"]
 nb = len(boffs) - 1
 o32 = np.zeros((nb, 32), np.uint8)

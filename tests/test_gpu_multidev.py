@@ -1,6 +1,7 @@
 """The library's multi-device host paths on a one-GPU box: NWC_VIRTUAL_DEVICES=k (3, and 8 = one
 node's width) makes nwc_init open k contexts on the GPU, so nwc_verify_strict_many's shard threads and bitmap merge,
-nwc_verify_batch_many's certificate cuts and nwc_sha512_trunc32_many's split all run as with three
+nwc_verify_batch_many's and nwc_verify_batch_straus_many's certificate cuts and nwc_sha512_trunc32_many's
+split all run as with three
 GPUs.  Outputs must equal the oracle's bit for bit, including verdicts that
 straddle the shard boundaries."""
 import hashlib
@@ -58,6 +59,9 @@ def test_contexts_match_oracle(oracle, tmp_path, contexts):
     ocert, obad = oracle.batch_many(dig, offs, vp, vs)
     assert (bits(got2["cert"], len(sizes)) == ocert).all()
     assert (bits(got2["bad"], n) == obad).all() and obad.sum() >= flip.sum()
+    # the Straus host entry over the same certificate cuts (honest keys: the deterministic domain)
+    assert (bits(got2["cert_straus"], len(sizes)) == ocert).all()
+    assert (bits(got2["bad_straus"], n) == obad).all()
     raw = blob.tobytes()
     for i in range(len(lens)):
         assert got["digests"][i].tobytes() == hashlib.sha512(raw[boffs[i]:boffs[i + 1]]).digest()[:32], i

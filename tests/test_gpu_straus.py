@@ -111,3 +111,33 @@ def test_without_basepoint_comb_takes_the_leaves():
                         os.path.join(ROOT, "tests", "test_gpu_straus.py") + "::test_certificates_vs_oracle[383]"],
                        env=dict(os.environ, NWC_COMB16="0"), cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_host_entry_vs_oracle(oracle):
+    """nwc_verify_batch_straus_many (host buffers, the Rust shim's `verify_batch_many(.., true)`):
+    certificate verdicts and bad sets equal the oracle's and nwc_verify_batch_many's."""
+    import ctypes
+    from narwhal_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(43)
+    sizes = [0, 1, 3, 67, 67, 12, 13, 24, 100] + [int(x) for x in rng.integers(1, 90, 150)]
+    m = len(sizes)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    nv = int(offs[-1])
+    kseeds = rng.integers(0, 256, (120, 32), dtype=np.uint8)
+    dig = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    pks, sigs = oracle.keygen_sign_many(kseeds[rng.integers(0, 120, nv)], np.repeat(dig, sizes, axis=0))
+    bad = rng.random(nv) < 0.02
+    sigs[bad, 50] ^= 8
+    ocert, obad = oracle.batch_many(dig, offs, pks, sigs)
+    out = {}
+    for name in ("nwc_verify_batch_many", "nwc_verify_batch_straus_many"):
+        cert = ctypes.create_string_buffer((m + 7) // 8)
+        badb = ctypes.create_string_buffer((nv + 7) // 8)
+        _lib.check(getattr(lib, name)(_lib.buf(dig), _lib.buf(offs), _lib.buf(pks), _lib.buf(sigs), m, cert, badb))
+        out[name] = (np.unpackbits(np.frombuffer(cert.raw, np.uint8), bitorder="little")[:m].astype(bool),
+                     np.unpackbits(np.frombuffer(badb.raw, np.uint8), bitorder="little")[:nv].astype(bool))
+    for name, (c, b) in out.items():
+        assert (c == ocert).all(), name
+        assert (b == obad).all(), name
+    assert ocert.sum() > 20 and (~ocert).sum() > 20
