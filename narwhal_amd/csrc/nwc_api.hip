@@ -215,6 +215,9 @@ struct DevCtx {
 #ifndef NWC_HOST_CHUNK
 #define NWC_HOST_CHUNK (1u << 17)
 #endif
+#ifndef NWC_HOST_CHUNK_GROWTH
+#define NWC_HOST_CHUNK_GROWTH 3
+#endif
 #ifndef NWC_PINNED_STAGE_MAX
 #define NWC_PINNED_STAGE_MAX (1u << 20)
 #endif
@@ -933,11 +936,24 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     const char* e = std::getenv("NWC_HOST_CHUNK");   // 0 = no pipelining (A/B)
     return e ? (uint64_t)std::strtoull(e, nullptr, 10) / 64 * 64 : (uint64_t)NWC_HOST_CHUNK;
   }();
+  static const uint64_t growth = [] {
+    const char* e = std::getenv("NWC_HOST_CHUNK_GROWTH");   // 1 = equal chunks (A/B)
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)NWC_HOST_CHUNK_GROWTH;
+  }();
   if (chunk && n >= 2 * chunk) {
     // pipelined: inputs of chunk k on the transfer stream, its verification on the device stream
-    // after the chunk's event; every chunk has its own region of the arena (no reuse hazards)
+    // after the chunk's event; every chunk has its own region of the arena (no reuse hazards).
+    // Chunk k + 1 is up to `growth` x chunk k: its 128 B per equation cross PCIe (~50 GB/s) while
+    // chunk k verifies (~100 M/s), so it arrives in time while growing up to ~3.7x; fewer, larger
+    // launches leave fewer kernel tails (the first chunk is one round of resident lanes).
     if (!d.xfer) HIP_TRY(hipStreamCreateWithFlags(&d.xfer, hipStreamNonBlocking));
-    const uint64_t nch = (n + chunk - 1) / chunk;
+    std::vector<uint64_t> cuts{0};
+    for (uint64_t len = chunk; cuts.back() < n; len *= growth) {
+      uint64_t next = std::min<uint64_t>(n, cuts.back() + len);
+      if (n - next < chunk / 2) next = n;   // no sliver of a last chunk
+      cuts.push_back(next);
+    }
+    const uint64_t nch = cuts.size() - 1;
     while (d.ev_chunk.size() < nch) {
       hipEvent_t e;
       HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -949,7 +965,7 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     if (msg_index) HIP_TRY(hipMemcpyAsync(dm, msgs, msg_bytes, hipMemcpyHostToDevice, d.xfer));
     else if (!msg_stride) HIP_TRY(hipMemcpyAsync(dm, msgs, 32, hipMemcpyHostToDevice, d.xfer));
     for (uint64_t k = 0; k < nch; ++k) {
-      const uint64_t c0 = k * chunk, len = std::min<uint64_t>(chunk, n - c0);
+      const uint64_t c0 = cuts[k], len = cuts[k + 1] - cuts[k];
       if (msg_index) HIP_TRY(hipMemcpyAsync(dmi + c0, msg_index + lo + c0, 4 * len, hipMemcpyHostToDevice, d.xfer));
       else if (msg_stride) HIP_TRY(hipMemcpyAsync(dm + 32 * c0, msgs + 32 * (lo + c0), 32 * len, hipMemcpyHostToDevice, d.xfer));
       HIP_TRY(hipMemcpyAsync(dp + 32 * c0, pks + 32 * (lo + c0), 32 * len, hipMemcpyHostToDevice, d.xfer));
