@@ -646,10 +646,37 @@ def cpu_baseline_verify(msgs, pks, sigs, budget_s: float):
     v = orc.strict_many(m[:n], p[:n], s[:n], th)
     dt = time.perf_counter() - t0
     assert v.all(), "oracle rejected a valid signature"
-    return {"value": n / dt, "unit": "verifies/s", "cores": th, "kind": "port", "value_per_thread": n / dt / th,
-            "host": host_info(),
-            "sample": "%d of the cfg-2 triples (C restatement of dalek verify_strict, %d threads = every CPU the "
-                      "box grants this process, %.1f s)" % (n, th, dt)}
+    out = {"value": n / dt, "unit": "verifies/s", "cores": th, "kind": "port", "value_per_thread": n / dt / th,
+           "host": host_info(),
+           "sample": "%d of the cfg-2 triples (C restatement of dalek verify_strict, %d threads = every CPU the "
+                     "box grants this process, %.1f s)" % (n, th, dt)}
+    out["openssl"] = cpu_verify_openssl(m, p, s, th, budget_s / 2)
+    return out
+
+
+def cpu_verify_openssl(m, p, s, th: int, budget_s: float):
+    """SURVEY.md §8(d)'s optional third-party point: OpenSSL EVP Ed25519 single verification
+    (oracle/openssl_ed25519.c) on the same cfg-2 triples and threads. Not dalek semantics (it
+    accepts non-canonical and small-order encodings verify_strict rejects); on these honest
+    triples both accept, which the call asserts."""
+    from tests.oracle_lib import openssl_verify_many
+    k = 2048
+    t0 = time.perf_counter()
+    openssl_verify_many(m[:k], p[:k], s[:k], th)
+    dt = time.perf_counter() - t0
+    n = int(min(len(p), max(k, k * budget_s / max(dt, 1e-6))))
+    t0 = time.perf_counter()
+    v = openssl_verify_many(m[:n], p[:n], s[:n], th)
+    dt = time.perf_counter() - t0
+    assert v.all(), "OpenSSL rejected a valid signature"
+    return {"value": n / dt, "unit": "verifies/s", "cores": th, "kind": "third-party",
+            "semantics": "not dalek semantics (OpenSSL %s EVP Ed25519)" % openssl_version(),
+            "sample": "%d of the cfg-2 triples, %d threads, %.1f s" % (n, th, dt)}
+
+
+def openssl_version():
+    import ssl
+    return ssl.OPENSSL_VERSION.split()[1] if ssl.OPENSSL_VERSION.startswith("OpenSSL") else ssl.OPENSSL_VERSION
 
 
 def cpu_baseline_digest(budget_s: float):

@@ -115,6 +115,25 @@ class Oracle:
         return out
 
 
+OSSL_SO = os.path.join(ROOT, "oracle", "build", "libnwc_ossl.so")
+
+
+def openssl_verify_many(msgs: np.ndarray, pks: np.ndarray, sigs: np.ndarray, threads: int = 8) -> np.ndarray:
+    """OpenSSL EVP Ed25519 verification per triple (oracle/openssl_ed25519.c): bench.py's
+    third-party CPU point -- NOT dalek semantics (accepts what verify_strict rejects)."""
+    if not os.path.exists(OSSL_SO):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    lib = ctypes.CDLL(OSSL_SO)
+    vp = ctypes.c_void_p
+    lib.ossl_ed25519_verify_many.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
+    n = pks.shape[0]
+    out = np.zeros(n, dtype=np.uint8)
+    m, p, s = (np.ascontiguousarray(a, dtype=np.uint8) for a in (msgs, pks, sigs))
+    assert m.shape == (n, 32) and p.shape == (n, 32) and s.shape == (n, 64)
+    lib.ossl_ed25519_verify_many(Oracle._p(m), Oracle._p(p), Oracle._p(s), n, Oracle._p(out), threads)
+    return out.astype(bool)
+
+
 _ORACLE = None
 
 

@@ -69,6 +69,24 @@ def test_openssl_agrees_on_plain_cases(golden_verify):
     assert all(c["openssl"] == c["strict"] for c in checked)
 
 
+def test_openssl_bench_point(oracle, golden_verify):
+    """bench.py's third-party CPU point (oracle/openssl_ed25519.c, EVP Ed25519) reproduces the
+    fixture's OpenSSL verdicts on 32-byte messages and agrees with verify_strict on honest and
+    corrupted triples -- the bench workload's domain; elsewhere it is not dalek semantics."""
+    from tests.oracle_lib import openssl_verify_many
+    cases = [c for c in golden_verify["cases"] if "openssl" in c and len(c["msg"]) == 64]
+    assert cases
+    m, p, s = (np.array([list(bytes.fromhex(c[k])) for c in cases], np.uint8) for k in ("msg", "pk", "sig"))
+    assert list(openssl_verify_many(m, p, s, 2)) == [c["openssl"] for c in cases]
+    rng = np.random.default_rng(5)
+    n = 600
+    seeds, msgs = rng.integers(0, 256, (n, 32), np.uint8), rng.integers(0, 256, (n, 32), np.uint8)
+    pks, sigs = oracle.keygen_sign_many(seeds, msgs, 4)
+    sigs[::5, 3] ^= 0x10
+    got = openssl_verify_many(msgs, pks, sigs, 3)
+    assert (got == oracle.strict_many(msgs, pks, sigs, 4)).all() and got.sum() == n - len(range(0, n, 5))
+
+
 def test_c_oracle_batches(oracle, golden_batch):
     for b in golden_batch:
         msg = bytes.fromhex(b["msg"])
