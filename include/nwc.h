@@ -104,8 +104,8 @@ int nwc_auto_cache_info(uint32_t* capacity, uint64_t* builds, uint64_t* hits);
  * polled (the Processor stores the batch after hashing it anyway).  Digests come back in
  * submission order with the caller's tag.  One 500-KB batch alone takes ~28 ms on the GPU (a
  * sequential SHA-512 chain on one lane) against ~0.36 ms on one host core: measured, the GPU ties 16
- * host cores at ~1,000 batches per group and is ~2.3x faster at 100,000 (PCIe-bound, ~36 GB/s;
- * INTEGRATION.md §4).  Data path: NWC_DIGEST_STAGES (4) pinned 32-MB stages filled by
+ * host cores at ~1,000 batches per group and is ~3.8x faster at 100,000 (PCIe-bound, ~40 GB/s;
+ * 54 GB/s from the receive arena below).  Data path: NWC_DIGEST_STAGES (4) pinned 32-MB stages filled by
  * NWC_DIGEST_COPY_THREADS (8) host threads.  create returns NULL on failure
  * (nwc_last_error); poll waits up to wait_us for at least one digest and reports a device error
  * of the drain thread (sticky); destroy digests what is queued, then frees the digester. */
@@ -115,6 +115,19 @@ int nwc_digester_submit(nwc_digester* q, const uint8_t* batch, size_t len, uint6
 int nwc_digester_poll(nwc_digester* q, size_t max, uint32_t wait_us, uint64_t* tags, uint8_t* digests32,
                       size_t* n_done);
 int nwc_digester_stats(nwc_digester* q, uint64_t* groups, uint64_t* batches, uint64_t* bytes);
+/* Receive arena: `bytes` of pinned host memory owned by the digester (freed by destroy), for a
+ * worker that receives batches straight into it (the network read's destination, instead of a
+ * Vec the Processor later hands over).  A group whose batches all lie in the arena, each placed
+ * at the previous one's offset + its length rounded up to 16 bytes (starts 16-byte aligned),
+ * skips the stage fill: each contiguous run of batches is one DMA from the arena into HBM (at most
+ * 1,024 runs per group; otherwise, or with any batch outside the arena, the group takes the stage
+ * path).  Batches stay borrowed as with any submit: do not overwrite a batch's bytes before its
+ * digest has been polled.  Create it before the first submit; a later call returns the same
+ * arena if `bytes` fits.  Returns NULL on failure (nwc_last_error).  No counterpart in the
+ * reference (its Processor gets a Vec<u8>). */
+uint8_t* nwc_digester_arena(nwc_digester* q, size_t bytes);
+/* Groups that took the arena's direct path so far (diagnostics). */
+int nwc_digester_direct_groups(nwc_digester* q, uint64_t* direct_groups);
 int nwc_digester_destroy(nwc_digester* q);
 
 /* ---- primary messages ---------------------------------------- */

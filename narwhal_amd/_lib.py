@@ -69,6 +69,8 @@ _SIGS = {
                                          ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]),
     "nwc_digester_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_digester_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "nwc_digester_arena": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_size_t]),
+    "nwc_digester_direct_groups": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_shard_bounds": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "nwc_cert_cuts": (ctypes.c_int, [_c_u8p, ctypes.c_size_t, ctypes.c_uint32, _c_u8p]),

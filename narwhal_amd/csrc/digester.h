@@ -15,6 +15,7 @@
 // serialise with verification calls on the device's context).  Included by nwc_api.hip.
 #pragma once
 #include <array>
+#include <atomic>
 #include <functional>
 #include <condition_variable>
 #include <deque>
@@ -90,7 +91,7 @@ struct Digester {
   int err = 0;
   std::string err_msg;
   bool stop = false;
-  uint64_t groups = 0, batches = 0, bytes = 0;
+  uint64_t groups = 0, batches = 0, bytes = 0, submitted = 0;
   std::thread th;
   CopyPool pool;
   // device side (touched by the drain thread only)
@@ -107,6 +108,12 @@ struct Digester {
   size_t k_cap = 0;
   uint64_t* hse = nullptr;        // pinned starts/ends
   uint8_t* hout = nullptr;        // pinned digests
+  // receive arena (nwc_digester_arena): pinned host memory the caller writes batches into; a group
+  // whose batches all lie in it, packed at 16-byte-rounded strides, is DMA'd without a stage fill
+  uint8_t* arena = nullptr;
+  size_t arena_size = 0;
+  std::atomic<uint64_t> direct_groups{0};
+  static constexpr size_t MAX_DIRECT_RUNS = 1024;
 
   int init() {
     pool.start(copy_threads);
@@ -133,6 +140,7 @@ struct Digester {
     if (dout) (void)hipFree(dout);
     if (hse) (void)hipHostFree(hse);
     if (hout) (void)hipHostFree(hout);
+    if (arena) (void)hipHostFree(arena);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -166,16 +174,41 @@ struct Digester {
       HIP_TRY(hipMalloc(&ddata, cap));
       ddata_cap = cap;
     }
-    // gather through the two pinned stages: fill one (with copy_threads host threads, each a
-    // contiguous byte range of the stage) while the other's DMA is in flight.  Stage s covers the
+    using clk = std::chrono::steady_clock;
+    double t_wait = 0, t_fill = 0;
+    const auto t_start = clk::now();
+    // direct path: every batch in the receive arena, consecutive batches at the device layout's
+    // spacing (runs of them are one DMA each, straight from the arena into HBM)
+    std::vector<std::pair<size_t, size_t>> runs;   // [first, last] non-empty batches of each run
+    bool direct = arena != nullptr;
+    for (size_t i = 0; direct && i < k; ++i) {
+      if (g[i].len == 0) continue;   // nothing to move; never breaks a run
+      const uint8_t* p = g[i].p;
+      if (!(p >= arena && (size_t)(p - arena) <= arena_size && g[i].len <= arena_size - (size_t)(p - arena))) {
+        direct = false;
+        break;
+      }
+      // a run continues while batch i sits where the device layout puts it relative to the run's first
+      if (!runs.empty() && (uint64_t)(p - g[runs.back().first].p) == hse[i] - hse[runs.back().first])
+        runs.back().second = i;
+      else if (runs.size() < MAX_DIRECT_RUNS)
+        runs.emplace_back(i, i);
+      else
+        direct = false;
+    }
+    if (direct) {
+      for (const auto& r : runs)   // the run's bytes, source and device at the same relative offsets
+        HIP_TRY(hipMemcpyAsync(ddata + hse[r.first], g[r.first].p, hse[k + r.second] - hse[r.first],
+                               hipMemcpyHostToDevice, stream));
+      ++direct_groups;
+    }
+    // gather through the pinned stages: fill one (with copy_threads host threads, each a
+    // contiguous byte range of the stage) while the others' DMA is in flight.  Stage s covers the
     // device layout's bytes [pos, pos + STAGE); batch i sits at hse[i] (16-byte aligned starts).
     int s = 0;
     bool used[MAX_STAGES] = {};
     size_t first = 0;   // first batch that may overlap the current stage
-    using clk = std::chrono::steady_clock;
-    double t_wait = 0, t_fill = 0;
-    const auto t_start = clk::now();
-    for (uint64_t pos = 0; pos < total; pos += STAGE) {
+    for (uint64_t pos = 0; !direct && pos < total; pos += STAGE) {
       const uint64_t end = std::min<uint64_t>(pos + STAGE, total);
       const auto t0 = clk::now();
       if (used[s]) HIP_TRY(hipEventSynchronize(stage_ev[s]));   // its previous DMA has landed
@@ -209,7 +242,10 @@ struct Digester {
     HIP_TRY(hipMemcpyAsync(hout, dout, 32 * k, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     std::memcpy(out32, hout, 32 * k);
-    if (timing)
+    if (timing && direct)
+      std::fprintf(stderr, "nwc digester: group %zu, %.1f MB (arena, %zu direct DMA runs): total %.2f ms\n", k,
+                   total / 1e6, runs.size(), std::chrono::duration<double>(clk::now() - t_start).count() * 1e3);
+    else if (timing)
       std::fprintf(stderr, "nwc digester: group %zu, %.1f MB: fill %.2f ms (%.1f GB/s), waits on DMA %.2f ms, total %.2f ms\n",
                    k, total / 1e6, t_fill * 1e3, total / std::max(t_fill, 1e-9) / 1e9, t_wait * 1e3,
                    std::chrono::duration<double>(clk::now() - t_start).count() * 1e3);
@@ -291,9 +327,31 @@ int nwc_digester_submit(nwc_digester* h, const uint8_t* batch, size_t len, uint6
     std::lock_guard<std::mutex> lk(q->mu);
     if (q->stop) return set_err(NWC_ERR_ARG, "digester is shutting down");
     q->in.push_back(Digester::Item{batch, len, tag});
+    ++q->submitted;
   }
   q->cv_in.notify_one();
   return 0;
+}
+
+uint8_t* nwc_digester_arena(nwc_digester* h, size_t bytes) {
+  auto* q = reinterpret_cast<Digester*>(h);
+  if (!q) { set_err(NWC_ERR_ARG, "null digester"); return nullptr; }
+  std::lock_guard<std::mutex> lk(q->mu);
+  if (q->arena) {
+    if (bytes > q->arena_size) { set_err(NWC_ERR_ARG, "the digester's arena exists with %zu bytes", q->arena_size); return nullptr; }
+    return q->arena;
+  }
+  if (bytes == 0) { set_err(NWC_ERR_ARG, "arena size must be > 0"); return nullptr; }
+  if (q->submitted) { set_err(NWC_ERR_ARG, "create the arena before the first submit"); return nullptr; }
+  // ordinary cached pages for the caller's writes (as the stages); the DMA engine reads them
+  const hipError_t e = hipHostMalloc(&q->arena, bytes, hipHostMallocNonCoherent);
+  if (e != hipSuccess) {
+    q->arena = nullptr;
+    set_err(NWC_ERR_DEVICE, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    return nullptr;
+  }
+  q->arena_size = bytes;
+  return q->arena;
 }
 
 int nwc_digester_poll(nwc_digester* h, size_t max, uint32_t wait_us, uint64_t* tags, uint8_t* digests32, size_t* n_done) {
@@ -322,6 +380,13 @@ int nwc_digester_stats(nwc_digester* h, uint64_t* groups, uint64_t* batches, uin
   if (groups) *groups = q->groups;
   if (batches) *batches = q->batches;
   if (bytes) *bytes = q->bytes;
+  return 0;
+}
+
+int nwc_digester_direct_groups(nwc_digester* h, uint64_t* direct_groups) {
+  auto* q = reinterpret_cast<Digester*>(h);
+  if (!q || !direct_groups) return set_err(NWC_ERR_ARG, "null argument");
+  *direct_groups = q->direct_groups.load();
   return 0;
 }
 

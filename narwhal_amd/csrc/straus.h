@@ -38,6 +38,9 @@ namespace nwc {
 #ifndef NWC_STRAUS_WAVES_PER_SIMD
 #define NWC_STRAUS_WAVES_PER_SIMD 2
 #endif
+#ifndef NWC_STRAUS_VOTE_MAJOR
+#define NWC_STRAUS_VOTE_MAJOR 0
+#endif
 constexpr int STRAUS_WAVES_PER_SIMD = NWC_STRAUS_WAVES_PER_SIMD;
 constexpr int STRAUS_MAX_PER_LANE = 16;
 // per vote in a lane's scratch: A's and R's 9-entry tables, then the digit strings (64 B), padded
@@ -54,7 +57,7 @@ struct StrausArgs {
   uint64_t runs;              // sub-batch r = votes [r nv / runs, (r + 1) nv / runs), <= STRAUS_MAX_PER_LANE each
   uint32_t seed[8];
   const ge_niels_pad* comb16; // radix-2^22 basepoint comb
-  uint8_t* scratch;           // lane_stride bytes per lane slot
+  uint8_t* scratch;           // lane_stride bytes per lane slot (vote-major: [vote of run][lane slot])
   uint64_t lane_stride;       // max votes per run * STRAUS_VOTE_BYTES
   uint64_t* leaf_words;       // bit v = vote v's sub-batch passed (zeroed by the caller)
   uint32_t* list;             // votes of the sub-batches that failed (for the exact leaves)
@@ -125,11 +128,18 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
   __shared__ u32 dl[STRAUS_LDS_WORDS];
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
+  // vote t of lane slot l: vote-major ([t][l], a wave's 64 lanes of one vote within 156 KB, as the
+  // leaf kernel's tables) or lane-major ([l][t], a wave's gather spread over 64 x lane_stride)
+#if NWC_STRAUS_VOTE_MAJOR
+  auto vote_base = [&](uint64_t t) { return a.scratch + (t * lanes + slot) * STRAUS_VOTE_BYTES; };
+#else
   uint8_t* const base = a.scratch + slot * a.lane_stride;
+  auto vote_base = [&](uint64_t t) { return base + t * STRAUS_VOTE_BYTES; };
+#endif
   // entry 0 (the identity) of the first vote's tables: the add every lane of a wave makes in a
   // (window, vote) step where it has no vote of its own reads it
-  LaneTable{reinterpret_cast<uint4*>(base)}.store(0, ge_cached_identity());
-  LaneTable{reinterpret_cast<uint4*>(base + TAB_BYTES_PER_LANE)}.store(0, ge_cached_identity());
+  LaneTable{reinterpret_cast<uint4*>(vote_base(0))}.store(0, ge_cached_identity());
+  LaneTable{reinterpret_cast<uint4*>(vote_base(0) + TAB_BYTES_PER_LANE)}.store(0, ge_cached_identity());
   // persistent: lane slot l takes sub-batches l, l + lanes, ...
   for (uint64_t r0 = slot; ; r0 += lanes) {
     // wave-uniform loop exit: every lane of the wave leaves together
@@ -156,7 +166,7 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
       sc_mul128(z, kw, zk);
       sc_mul128(z, sg + 8, zs);
       sc_add_l(S, zs, S);
-      uint8_t* vb = base + (size_t)t * STRAUS_VOTE_BYTES;
+      uint8_t* vb = vote_base(t);
       // digit strings: z k mod l (64 signed radix-16 digits), z (33 digits of a < 2^128 value)
       u32* dg = reinterpret_cast<u32*>(vb + 2 * TAB_BYTES_PER_LANE);
       {
@@ -193,7 +203,7 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
         // stage the next 8 windows' digit words (a lane without vote u stages digit 0 = +8 nibbles)
 #pragma unroll 1
         for (uint32_t u = 0; u < nw; ++u) {
-          const u32* dg = reinterpret_cast<const u32*>(base + (size_t)u * STRAUS_VOTE_BYTES + 2 * TAB_BYTES_PER_LANE);
+          const u32* dg = reinterpret_cast<const u32*>(vote_base(u) + 2 * TAB_BYTES_PER_LANE);
           const bool has = u < nq;
           dl[(2 * u) * 256 + threadIdx.x] = has ? dg[w >> 3] : 0x88888888u;
           dl[(2 * u + 1) * 256 + threadIdx.x] = has ? dg[8 + (w >> 3)] : 0x88888888u;
@@ -206,8 +216,7 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
       const uint32_t rs = w <= 32 ? 1u : 0u, nadd = nw << rs;
       auto entry = [&](uint32_t j, i32& d, LaneTable& tab) {
         const uint32_t u = j >> rs, kind = j & rs;
-        tab = LaneTable{reinterpret_cast<uint4*>(base + (size_t)(u < nq ? u : 0) * STRAUS_VOTE_BYTES +
-                                                 kind * TAB_BYTES_PER_LANE)};
+        tab = LaneTable{reinterpret_cast<uint4*>(vote_base(u < nq ? u : 0) + kind * TAB_BYTES_PER_LANE)};
         d = (i32)((dl[(2 * u + kind) * 256 + threadIdx.x] >> sh) & 15u) - 8;
       };
 #if NWC_PACKED_TABLES

@@ -61,6 +61,22 @@ class Digester:
         _lib.check(self.lib.nwc_digester_submit(self.h, buf, n, tag))
         return tag
 
+    def arena(self, nbytes: int):
+        """The digester's pinned receive arena (`nwc_digester_arena`) as a writable uint8 numpy
+        array (valid until close()).  Batches written into it back to back, each at the previous
+        one's offset + its length rounded up to 16, and submitted as views of it, are DMA'd straight
+        into HBM (no stage fill)."""
+        import numpy as np
+        p = self.lib.nwc_digester_arena(self.h, nbytes)
+        if not p:
+            raise _lib.DeviceError(self.lib.nwc_last_error().decode())
+        return np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+
+    def direct_groups(self) -> int:
+        n = ctypes.c_uint64()
+        _lib.check(self.lib.nwc_digester_direct_groups(self.h, ctypes.byref(n)))
+        return n.value
+
     def poll(self, max_n: int = 4096, wait_us: int = 0) -> List[Tuple[int, bytes]]:
         tags = (ctypes.c_uint64 * max_n)()
         digs = ctypes.create_string_buffer(32 * max_n)

@@ -43,6 +43,8 @@ extern "C" {
                              n_done: *mut usize) -> c_int;
     pub fn nwc_digester_stats(q: *mut nwc_digester, groups: *mut u64, batches: *mut u64, bytes: *mut u64) -> c_int;
     pub fn nwc_digester_destroy(q: *mut nwc_digester) -> c_int;
+    pub fn nwc_digester_arena(q: *mut nwc_digester, bytes: usize) -> *mut u8;
+    pub fn nwc_digester_direct_groups(q: *mut nwc_digester, direct_groups: *mut u64) -> c_int;
 
     pub fn nwc_dev_verify(d_msgs: *const c_void, d_msg_index: *const c_void, msg_stride: u64, d_pks: *const c_void,
                           d_sigs: *const c_void, n: u64, strict: c_int, d_verdict_words: *mut c_void,

@@ -123,3 +123,52 @@ def test_digester_stage_rotation(stages, threads):
         assert dg.stats()[0] == 1
     finally:
         dg.close()
+
+
+def test_digester_receive_arena():
+    """nwc_digester_arena: batches written into the pinned arena at 16-byte-rounded strides are
+    DMA'd straight into HBM (runs: a gap breaks a run, not the direct path); a group holding one
+    batch from outside the arena, or mis-spaced ones beyond the run limit, takes the stage path.
+    Digests equal hashlib either way, in submission order."""
+    from narwhal_amd.processor import Digester
+    rng = np.random.default_rng(9)
+    lens = [0, 1, 15, 16, 17, 127, 128, 129, 4096, 0, 333] + [int(x) for x in rng.integers(0, 400_000, 40)]
+    r16 = lambda n: (n + 15) & ~15  # noqa: E731
+    size = sum(r16(n) for n in lens) + (8 << 20)
+    dg = Digester(4096, 2_000_000)
+    try:
+        arena = dg.arena(size)
+        assert dg.arena(size // 2) is not None        # same arena again when it fits
+
+        def place(gap_at=None):
+            views, off = [], 0
+            for i, n in enumerate(lens):
+                if i == gap_at:
+                    off += 3 << 20                    # a ring wrap / hole: starts a new run
+                v = arena[off:off + n]
+                v[:] = rng.integers(0, 256, n, dtype=np.uint8)
+                views.append(v)
+                off += r16(n)
+            return views
+
+        def run(views, extra=None):
+            items = list(views) + ([extra] if extra is not None else [])
+            want = [_sha32(v) for v in items]
+            tags = [dg.submit(v) for v in items]
+            got = []
+            t0 = time.time()
+            while len(got) < len(items) and time.time() - t0 < 60:
+                got += dg.poll(4096, 200_000)
+            assert [t for t, _ in got] == tags
+            assert [d for _, d in got] == want
+
+        run(place())
+        d1 = dg.direct_groups()
+        assert d1 >= 1
+        run(place(gap_at=20))
+        d2 = dg.direct_groups()
+        assert d2 > d1
+        run(place(), extra=rng.integers(0, 256, 1000, dtype=np.uint8).tobytes())   # one batch outside
+        assert dg.direct_groups() == d2
+    finally:
+        dg.close()
