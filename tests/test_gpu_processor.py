@@ -170,5 +170,20 @@ def test_digester_receive_arena():
         assert d2 > d1
         run(place(), extra=rng.integers(0, 256, 1000, dtype=np.uint8).tobytes())   # one batch outside
         assert dg.direct_groups() == d2
+        # random spacing: batches packed at the 16-rounded stride, shifted by odd byte counts, or
+        # placed out of order -- every break starts a run; still direct, digests unchanged
+        views, off = [], 0
+        slots = []
+        for n in lens:
+            slots.append((off, n))
+            off += r16(n) + int(rng.choice([0, 0, 0, 1, 7, 4096]))
+        order = rng.permutation(len(slots))
+        for i in order:
+            o, n = slots[i]
+            v = arena[o:o + n]
+            v[:] = rng.integers(0, 256, n, dtype=np.uint8)
+        views = [arena[o:o + n] for o, n in (slots[i] for i in order)]
+        run(views)
+        assert dg.direct_groups() == d2 + 1
     finally:
         dg.close()
