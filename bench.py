@@ -14,10 +14,12 @@ correctness: every rank already holds its verdicts).
 
 Secondary leg (same JSON line, "digest"): BASELINE config 4, SHA-512[..32] of 100,000
 worker batches of 508,052 B (977 x 512-B txs, bincode WorkerMessage::Batch), hashed from a
-cycled pool of distinct batches resident in HBM.
+cycled pool of distinct batches resident in HBM.  `configs.cfg4_host` times the same batches
+from host memory through the worker's digester (pinned stages, and the pinned receive arena).
 
 cpu_baseline: the C restatement (oracle/, "port") of dalek verify_strict on the host cores of
-the GPU box (rank 0, N = 1 only), on a bounded sample of the same workload.
+the GPU box (rank 0, N = 1 only), on a bounded sample of the same workload, with OpenSSL's
+EVP Ed25519 beside it ("openssl", a third-party point, not dalek semantics).
 """
 from __future__ import annotations
 
@@ -750,6 +752,63 @@ def roofline_verify(vpc, n: int, kernel_ms: float, effective_tops: float):
 
 
 # ---- main ------------------------------------------------------------------------------------
+def bench_cfg4_host(group: int, pool: int = 256):
+    """Config 4 from host memory through the worker's digester (`nwc_digester_*`):
+    one group of `group` cfg-4 batches submitted at once, digests polled back -- from pageable
+    memory (gathered into pinned stages) and from the digester's pinned receive arena (one DMA
+    per group).  PCIe-inclusive; never the digest leg's value.  Every digest checked (hashlib)."""
+    import numpy as np
+    from narwhal_amd.processor import Digester
+    host = make_cfg4_pool(pool).cpu().numpy()
+    views = [host[b * CFG4_STRIDE:b * CFG4_STRIDE + CFG4_BATCH_BYTES] for b in range(pool)]
+    want = [hashlib.sha512(v).digest()[:32] for v in views]
+    r16 = (CFG4_BATCH_BYTES + 15) & ~15
+    out = {"workload": "%d cfg-4 batches per group from host memory, nwc_digester (H2D + digest + D2H)" % group}
+
+    def timed(dg, items):
+        import gc
+        ts = []
+        for _ in range(3):   # the first group sizes the digester's device buffers: not counted
+            gc.collect()
+            gc.disable()     # a collection inside the submit loop costs tens of ms of Python time
+            try:
+                t0 = time.perf_counter()
+                for i, v in enumerate(items):
+                    dg.submit(v, i)
+                t_sub = time.perf_counter() - t0
+                got = []
+                while len(got) < group:
+                    got += dg.poll(1 << 16, 1_000_000)
+                ts.append(time.perf_counter() - t0)
+            finally:
+                gc.enable()
+            assert [t for t, _ in got] == list(range(group)) and all(d == want[t % pool] for t, d in got)
+            out.setdefault("submit_ms", []).append(round(t_sub * 1e3, 2))
+        return min(ts[1:])
+
+    dg = Digester(group, 30_000_000)
+    try:
+        dt = timed(dg, [views[i % pool] for i in range(group)])
+    finally:
+        dg.close()
+    out["stages_GBps"], out["stages_ms"] = group * CFG4_BATCH_BYTES / dt / 1e9, dt * 1e3
+    dg = Digester(group, 30_000_000)
+    try:
+        arena = dg.arena(group * r16)
+        items = []
+        for i in range(group):
+            a = arena[i * r16:i * r16 + CFG4_BATCH_BYTES]
+            a[:] = views[i % pool]   # stands for the network read into the arena: not timed
+            items.append(a)
+        dt = timed(dg, items)
+        direct = dg.direct_groups()
+    finally:
+        dg.close()
+    out["arena_GBps"], out["arena_ms"], out["arena_direct_groups"] = group * CFG4_BATCH_BYTES / dt / 1e9, dt * 1e3, direct
+    out["parity_ok"] = True
+    return out
+
+
 def bench_cfg2_host_abi(lib, msgs, pks, sigs, reps: int):
     """Config 2 end to end ("plus a separate end-to-end time"): the same triples
     from pageable host memory through nwc_verify_strict_many (PCIe in, chunk-pipelined, verdict
@@ -790,6 +849,8 @@ def main():
     ap.add_argument("--cfg1-calls", type=int, default=10000, help="config 1 latency calls (0 = skip)")
     ap.add_argument("--wire-certs", type=int, default=20000, help="cfg 3 from wire bytes (0 = skip)")
     ap.add_argument("--cfg5-total", type=int, default=64 << 20, help="cfg 5 signatures over all ranks (0 = skip)")
+    ap.add_argument("--host-digest-group", type=int, default=8192,
+                    help="cfg 4 from host memory through nwc_digester: batches per group (0 = skip; needs --e2e-reps)")
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="cfg 2 end to end through the host ABI from pageable host buffers (0 = skip)")
     args = ap.parse_args()
@@ -872,6 +933,8 @@ def main():
     extras = {}
     if world == 1 and args.e2e_reps > 0:
         extras["cfg2_host_abi"] = bench_cfg2_host_abi(lib, msgs, pks, sigs, args.e2e_reps)
+    if world == 1 and args.e2e_reps > 0 and args.host_digest_group > 0:
+        extras["cfg4_host"] = bench_cfg4_host(args.host_digest_group)
     if args.cfg5_total > 0:
         extras["cfg5"] = bench_cfg5(lib, rank, world, args.cfg5_total, 2)
     if world == 1 and args.cfg3_certs > 0:

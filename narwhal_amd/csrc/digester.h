@@ -94,6 +94,7 @@ struct Digester {
   uint64_t groups = 0, batches = 0, bytes = 0, submitted = 0;
   std::thread th;
   CopyPool pool;
+  std::chrono::steady_clock::time_point t_group;   // first batch of the current group taken (timing)
   // device side (touched by the drain thread only)
   hipStream_t stream = nullptr;
   static constexpr size_t STAGE = 32u << 20;
@@ -243,11 +244,13 @@ struct Digester {
     HIP_TRY(hipStreamSynchronize(stream));
     std::memcpy(out32, hout, 32 * k);
     if (timing && direct)
-      std::fprintf(stderr, "nwc digester: group %zu, %.1f MB (arena, %zu direct DMA runs): total %.2f ms\n", k,
-                   total / 1e6, runs.size(), std::chrono::duration<double>(clk::now() - t_start).count() * 1e3);
+      std::fprintf(stderr, "nwc digester: group %zu, %.1f MB (arena, %zu direct DMA runs): gathered in %.2f ms, total %.2f ms\n", k,
+                   total / 1e6, runs.size(), std::chrono::duration<double>(t_start - t_group).count() * 1e3,
+                   std::chrono::duration<double>(clk::now() - t_start).count() * 1e3);
     else if (timing)
-      std::fprintf(stderr, "nwc digester: group %zu, %.1f MB: fill %.2f ms (%.1f GB/s), waits on DMA %.2f ms, total %.2f ms\n",
-                   k, total / 1e6, t_fill * 1e3, total / std::max(t_fill, 1e-9) / 1e9, t_wait * 1e3,
+      std::fprintf(stderr, "nwc digester: group %zu, %.1f MB: gathered in %.2f ms, fill %.2f ms (%.1f GB/s), waits on DMA %.2f ms, total %.2f ms\n",
+                   k, total / 1e6, std::chrono::duration<double>(t_start - t_group).count() * 1e3, t_fill * 1e3,
+                   total / std::max(t_fill, 1e-9) / 1e9, t_wait * 1e3,
                    std::chrono::duration<double>(clk::now() - t_start).count() * 1e3);
     return 0;
   }
@@ -264,6 +267,7 @@ struct Digester {
         if (in.empty()) return;   // stop, drained
         g.push_back(in.front());
         in.pop_front();
+        t_group = std::chrono::steady_clock::now();
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
         while (g.size() < max_group) {
           if (in.empty()) {
