@@ -652,7 +652,10 @@ def cpu_baseline_verify(msgs, pks, sigs, budget_s: float):
            "host": host_info(),
            "sample": "%d of the cfg-2 triples (C restatement of dalek verify_strict, %d threads = every CPU the "
                      "box grants this process, %.1f s)" % (n, th, dt)}
-    out["openssl"] = cpu_verify_openssl(m, p, s, th, budget_s / 2)
+    try:   # a third-party point: its absence must not cost the line
+        out["openssl"] = cpu_verify_openssl(m, p, s, th, budget_s / 2)
+    except Exception as e:  # noqa: BLE001
+        out["openssl"] = {"error": repr(e)}
     return out
 
 
@@ -934,7 +937,10 @@ def main():
     if world == 1 and args.e2e_reps > 0:
         extras["cfg2_host_abi"] = bench_cfg2_host_abi(lib, msgs, pks, sigs, args.e2e_reps)
     if world == 1 and args.e2e_reps > 0 and args.host_digest_group > 0:
-        extras["cfg4_host"] = bench_cfg4_host(args.host_digest_group)
+        try:   # 4.2 GB of pinned host memory: a box that refuses it still prints the line
+            extras["cfg4_host"] = bench_cfg4_host(args.host_digest_group)
+        except Exception as e:  # noqa: BLE001
+            extras["cfg4_host"] = {"error": repr(e)}
     if args.cfg5_total > 0:
         extras["cfg5"] = bench_cfg5(lib, rank, world, args.cfg5_total, 2)
     if world == 1 and args.cfg3_certs > 0:
