@@ -590,6 +590,33 @@ __device__ __forceinline__ ge_p1p1 add_lt_full(const ge_p1p1& t, const uint4 q[8
   r.T = fe_sub(zz2, tt);
   return r;
 }
+// add_lt that also gathers the NEXT addition's Y+X / Y-X (nab) right after its own last loads:
+// the add's final wait (in-order vmcnt) then leaves that gather in flight, and it lands during
+// this add's products (k_verify's ladder: the R add follows the A add with no doubling between).
+__device__ __forceinline__ ge_p1p1 add_lt_pf(const ge_p1p1& t, const LaneTable& tab, int e, bool neg,
+                                             const LaneTable& ntab, int ne, bool nneg, uint4 nab[4]) {
+  const fe qa = lt_load_fe(tab, e, neg ? 1 : 0);
+  const fe qb = lt_load_fe(tab, e, neg ? 0 : 1);
+  const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Z, t.Y);
+  const fe a = fe_add(Y3, X3), b = fe_sub(Y3, X3);
+  const fe Z3 = fe_mul(t.Z, t.T), T3 = fe_mul(t.X, t.Y);
+  __builtin_amdgcn_sched_barrier(0);
+  const fe qz = lt_load_fe(tab, e, 2);
+  const fe qt = lt_load_fe(tab, e, 3);
+  lt_load_ab(ntab, ne, nneg, nab);
+  __builtin_amdgcn_sched_barrier(0);
+  const fe pp = fe_mul(a, qa), mm = fe_mul(b, qb);
+  ge_p1p1 r;
+  r.X = fe_sub(pp, mm);
+  r.Y = fe_add(pp, mm);
+  const fe zz = fe_mul(Z3, qz);
+  const fe zz2 = fe_add(zz, zz);
+  fe tt = fe_mul(T3, qt);
+  tt = fe_select(tt, fe_neg(tt), neg);
+  r.Z = fe_add(zz2, tt);
+  r.T = fe_sub(zz2, tt);
+  return r;
+}
 #endif
 
 // tab[j] = j * P for j = 0..8 (tab[0] = identity)
@@ -802,6 +829,11 @@ typedef __attribute__((address_space(3))) void nwc_lvoid;
 #ifndef NWC_LADDER_PREFETCH
 #define NWC_LADDER_PREFETCH 0
 #endif
+// NWC_LADDER_R_PREFETCH: 1 = in the uncached ladder the R entry's Y+X / Y-X are gathered inside
+// the A add, after the A entry's own loads (add_lt_pf), instead of at the start of the R add
+#ifndef NWC_LADDER_R_PREFETCH
+#define NWC_LADDER_R_PREFETCH 0
+#endif
 // cache policy of the basepoint-entry DMA (random rows of the 2.1 GB tables, used once): 0 =
 // default, 2 = non-temporal (A/B: keep L2/MALL for the per-lane tables)
 #ifndef NWC_BASE_FETCH_CPOL
@@ -930,6 +962,18 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
     // after it then never wait on the DMA (vmcnt counts in order)
     const int nb = base_fetch(w, bd, d0, d1, T24, stage);
 #endif
+#if NWC_LADDER_R_PREFETCH && NWC_PACKED_TABLES && NWC_BASE_FETCH_EARLY
+    if (w != W - 1) {
+      ladder_dbl4(t);
+      da = digit16(bd, BD_C, w, W);
+      dr = digit16(bd, BD_D, w, W);
+      uint4 rab[4];
+      t = add_lt_pf(t, ta, da < 0 ? -da : da, da < 0, tr, dr < 0 ? -dr : dr, dr < 0, rab);
+      t = add_lt_ab(t, rab, tr, dr < 0 ? -dr : dr, dr < 0);
+    } else {
+      t = add_lt(t, tr, dr < 0 ? -dr : dr, dr < 0);
+    }
+#else
     if (w != W - 1) {
       ladder_dbl4(t);
       da = digit16(bd, BD_C, w, W);
@@ -940,6 +984,7 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
     const int nb = base_fetch(w, bd, d0, d1, T24, stage);
 #endif
     t = add_lt(t, tr, dr < 0 ? -dr : dr, dr < 0);
+#endif
     base_adds(t, nb, d0, d1, stage, T24);
   }
 #endif
