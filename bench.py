@@ -980,6 +980,9 @@ def main():
             "cpu_baseline": cpu,
             "digest": digest,
             "configs": extras,
+            # the hash of the sources libnwc.so was compiled from (narwhal_amd/build.py source_id)
+            "build_id": lib.nwc_build_id().decode(),
+            "memory": _lib.memory_info(),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

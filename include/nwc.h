@@ -45,6 +45,32 @@ const char* nwc_last_error(void);
 int nwc_version(void);
 /* Number of devices initialised. */
 int nwc_device_count(void);
+/* Identity of this build: a hash over the library's sources (narwhal_amd/csrc, this header)
+ * and compile flags, computed by narwhal_amd/build.py, so a caller or test can check that the
+ * binary it loaded was compiled from the tree it came with.  "unknown" for other builds. */
+const char* nwc_build_id(void);
+
+/* ---- device memory (a primary and a worker may share one GPU) ------------------------ */
+/* Bytes held by this process on the calling thread's device (nwc_dev_set_device): tables =
+ * basepoint tables built at nwc_init (radix-2^24 ladder tables 2.1 GB, radix-2^22 comb 3.2 GB
+ * unless NWC_COMB16=0, small ones); committee = the nwc_set_committee cache (20 MB per key with
+ * combs); auto_cache = the auto key cache (NWC_AUTO_KEYS); scratch = per-launch buffers grown on
+ * demand (ladder tables, Straus tables, staging, message buffers); digesters = the device buffers
+ * of live nwc_digesters on this device; device_free / device_total = hipMemGetInfo. */
+typedef struct nwc_memory {
+  uint64_t tables, committee, auto_cache, scratch, digesters, device_free, device_total;
+} nwc_memory;
+int nwc_memory_info(nwc_memory* out);
+/* Frees the calling thread's device's on-demand scratch (re-allocated by the next call that
+ * needs it); waits for the device to be idle.  Tables and caches stay. */
+int nwc_trim(void);
+
+/* Test / A-B knobs, settable at run time instead of through the environment (which is read
+ * once): "straus_nq" = votes per sub-batch of nwc_dev_verify_batch_straus (1..16, default 12,
+ * env NWC_STRAUS_NQ); "force_windows" = half-ladder windows forced on every wave (33..37, 0 = off,
+ * env NWC_FORCE_WINDOWS; verdicts must not change).  NWC_ERR_ARG for an unknown name or value.
+ * Not part of the crate's API. */
+int nwc_diag_set(const char* name, int64_t value);
 
 /* ---- verification ----------------------------------------------------------------------- */
 /* crypto::Signature::verify -> dalek verify_strict.  Replaces crypto/src/lib.rs:200-204
@@ -106,9 +132,15 @@ int nwc_auto_cache_info(uint32_t* capacity, uint64_t* builds, uint64_t* hits);
  * sequential SHA-512 chain on one lane) against ~0.36 ms on one host core: measured, the GPU ties 16
  * host cores at ~1,000 batches per group and is ~3.8x faster at 100,000 (PCIe-bound, ~40 GB/s;
  * 54 GB/s from the receive arena below).  Data path: NWC_DIGEST_STAGES (4) pinned 32-MB stages filled by
- * NWC_DIGEST_COPY_THREADS (8) host threads.  create returns NULL on failure
- * (nwc_last_error); poll waits up to wait_us for at least one digest and reports a device error
- * of the drain thread (sticky); destroy digests what is queued, then frees the digester. */
+ * NWC_DIGEST_COPY_THREADS (8) host threads; one launch holds at most NWC_DIGEST_MAX_BYTES
+ * (16 GiB) of batches in HBM (larger groups are cut), and a device buffer above
+ * NWC_DIGEST_KEEP_BYTES (1 GiB) is freed after its group.  create returns NULL on failure
+ * (nwc_last_error).  poll waits up to wait_us for a result and returns one run of results with
+ * the same status: digests (returns 0), or the tags of a group that failed on the device (returns
+ * the error code < 0; digests32 zeroed) -- every submitted tag comes back exactly once, in order.
+ * After a failure submit refuses new batches, and poll returns the error (n_done = 0) once
+ * nothing is left to hand back.  destroy digests what is queued, wakes threads blocked in poll and
+ * waits for them to leave, then frees the digester (no call on it may start after destroy). */
 typedef struct nwc_digester nwc_digester;
 nwc_digester* nwc_digester_create(uint32_t max_group, uint32_t max_wait_us);
 int nwc_digester_submit(nwc_digester* q, const uint8_t* batch, size_t len, uint64_t tag);

@@ -30,6 +30,10 @@ _SIGS = {
     "nwc_last_error": (ctypes.c_char_p, []),
     "nwc_version": (ctypes.c_int, []),
     "nwc_device_count": (ctypes.c_int, []),
+    "nwc_build_id": (ctypes.c_char_p, []),
+    "nwc_memory_info": (ctypes.c_int, [ctypes.c_void_p]),
+    "nwc_trim": (ctypes.c_int, []),
+    "nwc_diag_set": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
     "nwc_verify_strict": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p]),
     "nwc_verify_batch": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p]),
     "nwc_verify_strict_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p]),
@@ -84,6 +88,27 @@ class DeviceError(RuntimeError):
     """A runtime/device/argument failure of libnwc (never an 'invalid signature')."""
 
 
+class Memory(ctypes.Structure):
+    """nwc_memory (include/nwc.h): device bytes this process holds on one device."""
+    _fields_ = [(name, ctypes.c_uint64) for name in
+                ("tables", "committee", "auto_cache", "scratch", "digesters", "device_free", "device_total")]
+
+    def as_dict(self):
+        return {name: int(getattr(self, name)) for name, _ in self._fields_}
+
+
+def memory_info() -> dict:
+    """nwc_memory_info of the calling thread's device."""
+    m = Memory()
+    check(load().nwc_memory_info(ctypes.byref(m)))
+    return m.as_dict()
+
+
+def diag_set(name: str, value: int) -> None:
+    """nwc_diag_set: a test / A-B knob ("straus_nq", "force_windows")."""
+    check(load().nwc_diag_set(name.encode(), value))
+
+
 def load(init: bool = True, device_mask: int = 0):
     """Load libnwc.so (and nwc_init it unless init=False). Raises if unavailable."""
     global _lib
@@ -126,6 +151,9 @@ def buf(b) -> ctypes.c_void_p:
     try:
         import numpy as np
         if isinstance(b, np.ndarray):
+            # the C side reads nbytes contiguous bytes from the first element
+            if not b.flags.c_contiguous:
+                raise TypeError("non-contiguous array: pass np.ascontiguousarray(a)")
             return ctypes.c_void_p(b.ctypes.data)
     except ImportError:
         pass

@@ -6,6 +6,7 @@
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -24,17 +25,41 @@ def sources():
                   [os.path.join(ROOT, "include", "nwc.h")])
 
 
+def source_id() -> str:
+    """Hash of the library's sources (contents and tree-relative names) and compile flags: the build
+    id libnwc.so embeds (nwc_build_id) and smoke() / tests check against the tree they run from."""
+    h = hashlib.sha256(" ".join(f for f in FLAGS if not f.startswith("-I")).encode())
+    for s in sources():
+        h.update(os.path.relpath(s, ROOT).encode() + b"\0")
+        with open(s, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:20]
+
+
+def embedded_id(path: str = OUT):
+    """The build id a built library carries ("NWC_BUILD_ID:<id>" in its bytes), or None."""
+    try:
+        blob = open(path, "rb").read()
+    except OSError:
+        return None
+    i = blob.find(b"NWC_BUILD_ID:")
+    if i < 0:
+        return None
+    j = blob.find(b"\0", i)
+    return blob[i + 13:j].decode(errors="replace")
+
+
 def up_to_date() -> bool:
-    if not os.path.exists(OUT):
-        return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(s) <= t for s in sources())
+    """The in-tree library is current iff it embeds the hash of the present sources (not by
+    mtime: a copied tree keeps the .so but not the timestamps' meaning)."""
+    return os.path.exists(OUT) and embedded_id(OUT) == source_id()
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", os.path.join(CSRC, "nwc_api.hip")]
+    cmd = ([HIPCC] + FLAGS + ['-DNWC_BUILD_ID="%s"' % source_id()] +
+           ["-o", OUT + ".tmp", os.path.join(CSRC, "nwc_api.hip")])
     if verbose:
         print("[narwhal_amd.build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

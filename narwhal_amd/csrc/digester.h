@@ -5,7 +5,14 @@
 // for many batches at once (one batch is a 3,970-block chain on one lane, ~30 ms), so
 // the device-side Processor drains its channel instead: a drain thread takes the first batch, then
 // whatever else arrives within `max_wait_us` (up to `max_group` batches), and digests the group with
-// one launch.  Results come back in submission order.
+// one launch.  Results come back in submission order.  A group that fails on the device comes
+// back too: its tags with the error code (never as digests), and the digester then refuses new
+// batches (the error is sticky, as a HIP context error is).
+//
+// Device memory: the group's bytes live in one device buffer, at most NWC_DIGEST_MAX_BYTES
+// (16 GiB) per launch -- a larger group is cut into launches of at most that size -- and a buffer
+// larger than NWC_DIGEST_KEEP_BYTES (1 GiB) is released after its group, so one 100k-batch group
+// does not keep 50 GB resident (nwc_memory_info reports what a digester holds).
 //
 // Data path per group: the borrowed batches are gathered into NWC_DIGEST_STAGES (4) pinned 32-MB
 // stages in rotation (16-byte-aligned starts, the kernel's dwordx4 path; each stage filled by a
@@ -78,20 +85,24 @@ struct CopyPool {
 };
 
 struct Digester {
-  struct Item { const uint8_t* p; size_t len; uint64_t tag; };
+  struct Item { const uint8_t* p; size_t len; uint64_t tag; int status = 0; };
   uint32_t max_group, max_wait_us;
   int hip_id;
+  size_t max_bytes = (size_t)16 << 30;   // device bytes per launch (NWC_DIGEST_MAX_BYTES)
+  size_t keep_bytes = (size_t)1 << 30;   // device buffer kept between groups (NWC_DIGEST_KEEP_BYTES)
+  uint64_t fail_group = 0;               // test hook (NWC_DIGEST_FAIL_GROUP): group k (1-based) fails
   unsigned copy_threads = 8;        // host threads filling a pinned stage (NWC_DIGEST_COPY_THREADS)
   bool timing = false;              // NWC_DIGEST_TIMING: per-group fill / DMA-wait times on stderr
   std::mutex mu;
-  std::condition_variable cv_in, cv_out;
+  std::condition_variable cv_in, cv_out, cv_idle;
+  unsigned pollers = 0;            // threads inside nwc_digester_poll (destroy waits for them)
   std::deque<Item> in;
-  std::deque<Item> out;            // tag + digest (p unused)
+  std::deque<Item> out;            // tag + status + digest (p unused)
   std::deque<std::array<uint8_t, 32>> out_dig;
   int err = 0;
   std::string err_msg;
   bool stop = false;
-  uint64_t groups = 0, batches = 0, bytes = 0, submitted = 0;
+  uint64_t groups = 0, batches = 0, bytes = 0, submitted = 0, launched = 0;
   std::thread th;
   CopyPool pool;
   std::chrono::steady_clock::time_point t_group;   // first batch of the current group taken (timing)
@@ -103,10 +114,10 @@ struct Digester {
   uint8_t* stage[MAX_STAGES] = {};
   hipEvent_t stage_ev[MAX_STAGES] = {};
   uint8_t* ddata = nullptr;
-  size_t ddata_cap = 0;
+  std::atomic<size_t> ddata_cap{0};
   uint64_t* dse = nullptr;        // starts then ends
   uint8_t* dout = nullptr;
-  size_t k_cap = 0;
+  std::atomic<size_t> k_cap{0};
   uint64_t* hse = nullptr;        // pinned starts/ends
   uint8_t* hout = nullptr;        // pinned digests
   // receive arena (nwc_digester_arena): pinned host memory the caller writes batches into; a group
@@ -145,9 +156,13 @@ struct Digester {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
+  // device bytes the batch takes in a group's buffer (16-byte aligned starts)
+  static uint64_t padded(size_t len) { return (len + 15) & ~(uint64_t)15; }
+
   // SHA-512[..32] of every batch of the group into out32 (32 bytes each)
   int digest_group(const std::vector<Item>& g, uint8_t* out32) {
     const size_t k = g.size();
+    if (fail_group && ++launched == fail_group) return set_err(NWC_ERR_DEVICE, "injected digester failure (NWC_DIGEST_FAIL_GROUP)");
     if (k > k_cap) {
       const size_t nk = std::max(k, 2 * k_cap);
       if (dse) HIP_TRY(hipFree(dse));
@@ -165,13 +180,14 @@ struct Digester {
     for (size_t i = 0; i < k; ++i) {
       hse[i] = total;
       hse[k + i] = total + g[i].len;
-      total += (g[i].len + 15) & ~(uint64_t)15;
+      total += padded(g[i].len);
     }
     if (total + 16 > ddata_cap) {
       if (ddata) HIP_TRY(hipFree(ddata));
       ddata = nullptr;
       ddata_cap = 0;
-      const size_t cap = (total + 16) + (total + 16) / 4;
+      // headroom for slightly larger groups, but never past the per-launch cap
+      const size_t cap = std::max<size_t>(total + 16, std::min<size_t>((total + 16) + (total + 16) / 4, max_bytes + 16));
       HIP_TRY(hipMalloc(&ddata, cap));
       ddata_cap = cap;
     }
@@ -243,6 +259,11 @@ struct Digester {
     HIP_TRY(hipMemcpyAsync(hout, dout, 32 * k, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     std::memcpy(out32, hout, 32 * k);
+    if (ddata_cap > keep_bytes) {   // a large group's buffer is not kept resident
+      HIP_TRY(hipFree(ddata));
+      ddata = nullptr;
+      ddata_cap = 0;
+    }
     if (timing && direct)
       std::fprintf(stderr, "nwc digester: group %zu, %.1f MB (arena, %zu direct DMA runs): gathered in %.2f ms, total %.2f ms\n", k,
                    total / 1e6, runs.size(), std::chrono::duration<double>(t_start - t_group).count() * 1e3,
@@ -267,6 +288,7 @@ struct Digester {
         if (in.empty()) return;   // stop, drained
         g.push_back(in.front());
         in.pop_front();
+        uint64_t gbytes = padded(g.back().len);
         t_group = std::chrono::steady_clock::now();
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
         while (g.size() < max_group) {
@@ -275,6 +297,9 @@ struct Digester {
             if (!cv_in.wait_until(lk, deadline, [&] { return stop || !in.empty(); })) break;
             if (in.empty()) break;
           }
+          // one launch's device bytes stay under max_bytes (a single larger batch goes alone)
+          if (gbytes + padded(in.front().len) > max_bytes) break;
+          gbytes += padded(in.front().len);
           g.push_back(in.front());
           in.pop_front();
         }
@@ -282,15 +307,15 @@ struct Digester {
       dig.resize(32 * g.size());
       const int rc = digest_group(g, dig.data());
       std::lock_guard<std::mutex> lk(mu);
-      if (rc) {
-        if (!err) { err = rc; err_msg = t_err; }
-      } else {
-        ++groups;
-        for (size_t i = 0; i < g.size(); ++i) {
-          out.push_back(Item{nullptr, g[i].len, g[i].tag});
-          std::array<uint8_t, 32> a;
-          std::memcpy(a.data(), dig.data() + 32 * i, 32);
-          out_dig.push_back(a);
+      if (rc && !err) { err = rc; err_msg = t_err; }
+      if (!rc) ++groups;
+      // every tag comes back, in order: a failed group's with its error code and no digest
+      for (size_t i = 0; i < g.size(); ++i) {
+        out.push_back(Item{nullptr, g[i].len, g[i].tag, rc});
+        std::array<uint8_t, 32> a{};
+        if (!rc) std::memcpy(a.data(), dig.data() + 32 * i, 32);
+        out_dig.push_back(a);
+        if (!rc) {
           ++batches;
           bytes += g[i].len;
         }
@@ -299,6 +324,22 @@ struct Digester {
     }
   }
 };
+
+// live digesters (nwc_memory_info reports their device buffers per device)
+std::mutex g_dg_mu;
+std::vector<Digester*> g_digesters;
+void digester_register(Digester* q, bool add) {
+  std::lock_guard<std::mutex> lk(g_dg_mu);
+  if (add) g_digesters.push_back(q);
+  else g_digesters.erase(std::remove(g_digesters.begin(), g_digesters.end(), q), g_digesters.end());
+}
+uint64_t digester_device_bytes(int hip_id) {
+  std::lock_guard<std::mutex> lk(g_dg_mu);
+  uint64_t b = 0;
+  for (const Digester* q : g_digesters)
+    if (q->hip_id == hip_id) b += q->ddata_cap.load() + 48 * (uint64_t)q->k_cap.load();
+  return b;
+}
 
 }  // namespace
 
@@ -314,12 +355,16 @@ nwc_digester* nwc_digester_create(uint32_t max_group, uint32_t max_wait_us) {
   if (const char* e = std::getenv("NWC_DIGEST_COPY_THREADS")) q->copy_threads = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("NWC_DIGEST_STAGES")) q->nstages = std::min(Digester::MAX_STAGES, std::max(2, std::atoi(e)));
   q->timing = std::getenv("NWC_DIGEST_TIMING") != nullptr;
+  if (const char* e = std::getenv("NWC_DIGEST_MAX_BYTES")) q->max_bytes = std::max<size_t>(1 << 20, std::strtoull(e, nullptr, 10));
+  if (const char* e = std::getenv("NWC_DIGEST_KEEP_BYTES")) q->keep_bytes = std::strtoull(e, nullptr, 10);
+  if (const char* e = std::getenv("NWC_DIGEST_FAIL_GROUP")) q->fail_group = std::strtoull(e, nullptr, 10);
   if (q->init()) {
     q->release();
     delete q;
     return nullptr;
   }
   q->th = std::thread([q] { q->run(); });
+  digester_register(q, true);
   return reinterpret_cast<nwc_digester*>(q);
 }
 
@@ -330,6 +375,7 @@ int nwc_digester_submit(nwc_digester* h, const uint8_t* batch, size_t len, uint6
   {
     std::lock_guard<std::mutex> lk(q->mu);
     if (q->stop) return set_err(NWC_ERR_ARG, "digester is shutting down");
+    if (q->err) return set_err(q->err, "digester failed earlier: %s", q->err_msg.c_str());
     q->in.push_back(Digester::Item{batch, len, tag});
     ++q->submitted;
   }
@@ -362,10 +408,13 @@ int nwc_digester_poll(nwc_digester* h, size_t max, uint32_t wait_us, uint64_t* t
   auto* q = reinterpret_cast<Digester*>(h);
   if (!q || !n_done || (max && (!tags || !digests32))) return set_err(NWC_ERR_ARG, "null argument");
   std::unique_lock<std::mutex> lk(q->mu);
-  if (wait_us && q->out.empty() && !q->err)
-    q->cv_out.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return !q->out.empty() || q->err; });
+  ++q->pollers;
+  if (wait_us && q->out.empty() && !q->err && !q->stop)
+    q->cv_out.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return !q->out.empty() || q->err || q->stop; });
+  // a run of results with one status: digests (rc 0) or a failed group's tags (rc < 0)
+  const int status = q->out.empty() ? 0 : q->out.front().status;
   size_t n = 0;
-  while (n < max && !q->out.empty()) {
+  while (n < max && !q->out.empty() && q->out.front().status == status) {
     tags[n] = q->out.front().tag;
     std::memcpy(digests32 + 32 * n, q->out_dig.front().data(), 32);
     q->out.pop_front();
@@ -373,8 +422,11 @@ int nwc_digester_poll(nwc_digester* h, size_t max, uint32_t wait_us, uint64_t* t
     ++n;
   }
   *n_done = n;
-  if (q->err) return set_err(q->err, "%s", q->err_msg.c_str());
-  return 0;
+  int rc = 0;
+  if (status) rc = set_err(status, "digest group failed: %s", q->err_msg.c_str());
+  else if (n == 0 && q->err) rc = set_err(q->err, "%s", q->err_msg.c_str());   // sticky, nothing left to hand back
+  if (--q->pollers == 0) q->cv_idle.notify_all();
+  return rc;
 }
 
 int nwc_digester_stats(nwc_digester* h, uint64_t* groups, uint64_t* batches, uint64_t* bytes) {
@@ -402,7 +454,14 @@ int nwc_digester_destroy(nwc_digester* h) {
     q->stop = true;
   }
   q->cv_in.notify_all();
+  q->cv_out.notify_all();   // a poller blocked on an empty queue returns now
   if (q->th.joinable()) q->th.join();
+  {
+    // no thread may still be inside poll when the digester is freed
+    std::unique_lock<std::mutex> lk(q->mu);
+    q->cv_idle.wait(lk, [&] { return q->pollers == 0; });
+  }
+  digester_register(q, false);
   const int rc = q->err;
   q->release();
   delete q;

@@ -55,10 +55,6 @@ FE_DEV fe fe_select(const fe& a, const fe& b, bool c) {
 FE_DEV i64 fe_col_bias(int k) { return (k & 1) ? ((i64)1 << 24) : ((i64)1 << 25); }
 
 FE_DEV fe fe_carry_wide(i64 h[10]) {
-#if NWC_EXPERIMENT_NO_CARRY
-  // timing experiment only (wrong results): the carry chain's share of the kernel time
-  { fe o; _Pragma("unroll") for (int i = 0; i < 10; ++i) o.v[i] = (i32)(h[i] >> 26); return o; }
-#endif
   i64 c;
   u32 r[10];
 #define FE_FLOOR(i, sh) { c = h[i] >> sh; r[i] = (u32)h[i] & ((1u << sh) - 1u); }

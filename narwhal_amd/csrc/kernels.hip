@@ -30,28 +30,13 @@
 #include "fe_sliced.h"
 #include "ge_sliced.h"
 
-// Build switches of the half-size ladder (A/B experiments, profiles/r02/experiments.md):
-//   NWC_BASE_FETCH_EARLY  issue a window's first basepoint DMA before its doublings (1) or after
-//                         the A add (0)
-//   NWC_ADD_LT_SPLIT      add_lt gathers Z and 2dT only after the extended form is built (1) or
-//                         all four coordinates up front (0)
-#ifndef NWC_BASE_FETCH_EARLY
-#define NWC_BASE_FETCH_EARLY 1
-#endif
-#ifndef NWC_ADD_LT_SPLIT
-#define NWC_ADD_LT_SPLIT 1
-#endif
-//   NWC_PROLOGUE_LOOP     uncached half-size path: scalars first, then R and A decoded in a rolled
-//                         two-iteration loop, each table written at once (1); or both points
-//                         decoded by a noinline call and held through scratch memory (0, round 2)
-#ifndef NWC_PROLOGUE_LOOP
-#define NWC_PROLOGUE_LOOP 0
-#endif
-//   NWC_PACKED_TABLES     per-lane ladder tables with 128-B entries (limbs packed, one cache line
-//                         per gather) (1) or 160-B entries of plain limbs (0)
-#ifndef NWC_PACKED_TABLES
-#define NWC_PACKED_TABLES 1
-#endif
+// Layout and scheduling choices of the half-size ladder were settled by interleaved A/B builds
+// (profiles/r02/experiments.md, profiles/r03/experiments.md); the rejected variants live in git
+// history and those logs, not as build switches here:
+//   - the window's first basepoint DMA is issued before its doublings;
+//   - add_lt gathers Z and 2dT only after the extended form is built;
+//   - per-lane ladder tables hold 128-B packed entries (one cache line per gather);
+//   - R and A are decoded by one noinline call whose points return through scratch.
 
 namespace nwc {
 
@@ -384,12 +369,11 @@ __global__ void k_build_comb16(ge_niels_pad* __restrict__ out, const ge_p3* __re
 }
 
 // ------------------------------------------------------------------------------- ladder
-// Per-lane table of the variable base in global scratch, lane-contiguous: 9 entries x 160 B
-// (cached point = 40 dwords = 10 x dwordx4).  A lookup reads one lane's 160 contiguous bytes,
-// so a wave touches ~128 lines per lookup instead of the whole wave's table (the compiler's
+// Per-lane table of the variable base in global scratch, lane-contiguous: 9 entries x 128 B
+// (a cached point packed into 8 x dwordx4).  A lookup reads one lane's 128 contiguous bytes,
+// so a wave touches ~64 lines per lookup instead of the whole wave's table (the compiler's
 // private memory interleaves lanes dword by dword).
 constexpr int TAB_ENTRIES = 9;
-#if NWC_PACKED_TABLES
 // Packed entries: each coordinate's ten limbs, made non-negative, in 32 bytes (fields of 26, 26,
 // 26, 25, 26, 25, 26, 25, 26, 25 bits at bit offsets 0, 26, 52, 78, 103, 129, 154, 180, 205, 231;
 // limb 1 keeps one slack bit for the final carry).  An entry is 128 B on a 128-B boundary, so a
@@ -437,14 +421,10 @@ __device__ __forceinline__ fe fe_unpack(const uint4& lo, const uint4& hi) {
   r.v[9] = (i32)(hi.w >> 7);
   return r;
 }
-#else
-constexpr int TAB_U4_PER_ENTRY = 10;
-#endif
 constexpr size_t TAB_BYTES_PER_LANE = TAB_ENTRIES * TAB_U4_PER_ENTRY * 16;   // 1440 (1152 packed)
 
 struct LaneTable {
   uint4* p;
-#if NWC_PACKED_TABLES
   __device__ __forceinline__ void store(int e, const ge_cached& c) const {
     const fe* co = &c.YpX;
     _Pragma("unroll") for (int k = 0; k < 4; ++k) {
@@ -460,47 +440,21 @@ struct LaneTable {
     _Pragma("unroll") for (int k = 0; k < 4; ++k) co[k] = fe_unpack(p[e * 8 + 2 * k], p[e * 8 + 2 * k + 1]);
     return c;
   }
-#else
-  __device__ __forceinline__ void store(int e, const ge_cached& c) const {
-    const uint4* src = reinterpret_cast<const uint4*>(&c);
-    _Pragma("unroll") for (int i = 0; i < TAB_U4_PER_ENTRY; ++i) p[e * TAB_U4_PER_ENTRY + i] = src[i];
-  }
-  __device__ __forceinline__ ge_cached load(int e) const {
-    ge_cached c;
-    uint4* dst = reinterpret_cast<uint4*>(&c);
-    _Pragma("unroll") for (int i = 0; i < TAB_U4_PER_ENTRY; ++i) dst[i] = p[e * TAB_U4_PER_ENTRY + i];
-    return c;
-  }
-#endif
 };
-static_assert(NWC_PACKED_TABLES || sizeof(ge_cached) == TAB_U4_PER_ENTRY * 16, "cached point layout");
 
 // Coordinate k (0 YpX, 1 YmX, 2 Z, 3 T2d) of entry e: 40 bytes at an 8-byte-aligned offset
 // (packed: 32 bytes at a 32-byte-aligned offset).
 __device__ __forceinline__ fe lt_load_fe(const LaneTable& tab, int e, int k) {
-#if NWC_PACKED_TABLES
   return fe_unpack(tab.p[e * 8 + 2 * k], tab.p[e * 8 + 2 * k + 1]);
-#else
-  const uint2* q = reinterpret_cast<const uint2*>(tab.p) + e * 20 + k * 5;
-  fe r;
-  _Pragma("unroll") for (int i = 0; i < 5; ++i) {
-    const uint2 v = q[i];
-    r.v[2 * i] = (i32)v.x;
-    r.v[2 * i + 1] = (i32)v.y;
-  }
-  return r;
-#endif
 }
 // The ladder's first entry as a completed point: the table's coordinates re-centred first when
 // packed (2Z of limbs up to 2^27 would exceed the multiplier's right-operand bound).
 __device__ __forceinline__ ge_cached lt_first(const LaneTable& tab, int e) {
   ge_cached c = tab.load(e);
-#if NWC_PACKED_TABLES
   c.YpX = fe_tighten(c.YpX);
   c.YmX = fe_tighten(c.YmX);
   c.Z = fe_tighten(c.Z);
   c.T2d = fe_tighten(c.T2d);
-#endif
   return c;
 }
 
@@ -514,9 +468,7 @@ __device__ __forceinline__ ge_p1p1 add_lt(const ge_p1p1& t, const LaneTable& tab
   const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Z, t.Y);
   const fe a = fe_add(Y3, X3), b = fe_sub(Y3, X3);
   const fe Z3 = fe_mul(t.Z, t.T), T3 = fe_mul(t.X, t.Y);
-#if NWC_ADD_LT_SPLIT
   __builtin_amdgcn_sched_barrier(0);
-#endif
   const fe qz = lt_load_fe(tab, e, 2);
   const fe qt = lt_load_fe(tab, e, 3);
   const fe pp = fe_mul(a, qa), mm = fe_mul(b, qb);
@@ -532,36 +484,13 @@ __device__ __forceinline__ ge_p1p1 add_lt(const ge_p1p1& t, const LaneTable& tab
   return r;
 }
 
-#if NWC_PACKED_TABLES
-// add_lt with the entry's first two coordinates (Y+X, Y-X, swapped when neg) already loaded --
-// packed, 4 x uint4 -- so a caller that knows its next digit can issue the gather one addition
-// ahead (k_verify_straus: consecutive additions with no doubling between them).
+// The entry's first two coordinates (Y+X, Y-X, swapped when neg), packed: 4 x uint4.
 __device__ __forceinline__ void lt_load_ab(const LaneTable& tab, int e, bool neg, uint4 ab[4]) {
   const int ka = neg ? 1 : 0, kb = neg ? 0 : 1;
   ab[0] = tab.p[e * 8 + 2 * ka];
   ab[1] = tab.p[e * 8 + 2 * ka + 1];
   ab[2] = tab.p[e * 8 + 2 * kb];
   ab[3] = tab.p[e * 8 + 2 * kb + 1];
-}
-__device__ __forceinline__ ge_p1p1 add_lt_ab(const ge_p1p1& t, const uint4 ab[4], const LaneTable& tab, int e,
-                                             bool neg) {
-  const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Z, t.Y);
-  const fe a = fe_add(Y3, X3), b = fe_sub(Y3, X3);
-  const fe Z3 = fe_mul(t.Z, t.T), T3 = fe_mul(t.X, t.Y);
-  __builtin_amdgcn_sched_barrier(0);
-  const fe qz = lt_load_fe(tab, e, 2);
-  const fe qt = lt_load_fe(tab, e, 3);
-  const fe pp = fe_mul(a, fe_unpack(ab[0], ab[1])), mm = fe_mul(b, fe_unpack(ab[2], ab[3]));
-  ge_p1p1 r;
-  r.X = fe_sub(pp, mm);
-  r.Y = fe_add(pp, mm);
-  const fe zz = fe_mul(Z3, qz);
-  const fe zz2 = fe_add(zz, zz);
-  fe tt = fe_mul(T3, qt);
-  tt = fe_select(tt, fe_neg(tt), neg);
-  r.Z = fe_add(zz2, tt);
-  r.T = fe_sub(zz2, tt);
-  return r;
 }
 // The whole packed entry (Y+X, Y-X swapped when neg, Z, 2dT: 8 x uint4) gathered ahead of its
 // add, so that the add issues no load of its own: with a partial prefetch the add's own Z / 2dT
@@ -590,34 +519,6 @@ __device__ __forceinline__ ge_p1p1 add_lt_full(const ge_p1p1& t, const uint4 q[8
   r.T = fe_sub(zz2, tt);
   return r;
 }
-// add_lt that also gathers the NEXT addition's Y+X / Y-X (nab) right after its own last loads:
-// the add's final wait (in-order vmcnt) then leaves that gather in flight, and it lands during
-// this add's products (k_verify's ladder: the R add follows the A add with no doubling between).
-__device__ __forceinline__ ge_p1p1 add_lt_pf(const ge_p1p1& t, const LaneTable& tab, int e, bool neg,
-                                             const LaneTable& ntab, int ne, bool nneg, uint4 nab[4]) {
-  const fe qa = lt_load_fe(tab, e, neg ? 1 : 0);
-  const fe qb = lt_load_fe(tab, e, neg ? 0 : 1);
-  const fe X3 = fe_mul(t.X, t.T), Y3 = fe_mul(t.Z, t.Y);
-  const fe a = fe_add(Y3, X3), b = fe_sub(Y3, X3);
-  const fe Z3 = fe_mul(t.Z, t.T), T3 = fe_mul(t.X, t.Y);
-  __builtin_amdgcn_sched_barrier(0);
-  const fe qz = lt_load_fe(tab, e, 2);
-  const fe qt = lt_load_fe(tab, e, 3);
-  lt_load_ab(ntab, ne, nneg, nab);
-  __builtin_amdgcn_sched_barrier(0);
-  const fe pp = fe_mul(a, qa), mm = fe_mul(b, qb);
-  ge_p1p1 r;
-  r.X = fe_sub(pp, mm);
-  r.Y = fe_add(pp, mm);
-  const fe zz = fe_mul(Z3, qz);
-  const fe zz2 = fe_add(zz, zz);
-  fe tt = fe_mul(T3, qt);
-  tt = fe_select(tt, fe_neg(tt), neg);
-  r.Z = fe_add(zz2, tt);
-  r.T = fe_sub(zz2, tt);
-  return r;
-}
-#endif
 
 // tab[j] = j * P for j = 0..8 (tab[0] = identity)
 __device__ __forceinline__ void build_table(const LaneTable& tab, const ge_p3& P) {
@@ -815,36 +716,16 @@ __device__ __forceinline__ int base_window_digits(int w) {
 // latency hides behind ~2.6k VALU instructions and no VGPR holds the entry meanwhile.
 typedef __attribute__((address_space(1))) void nwc_gvoid;
 typedef __attribute__((address_space(3))) void nwc_lvoid;
-// NWC_STAGE_ENTRIES = 1 (default): an 8 KB stage per wave; the second entry of a window is
-// fetched after the first one has been read (it lands during the first Niels add).  Measured
-// +1.5 % verifies/s over a 16 KB two-entry stage (5 interleaved A/B pairs on two boxes,
-// profiles/r02/experiments.md), at the same occupancy (VGPR-bound to 2 waves per SIMD).
-#ifndef NWC_STAGE_ENTRIES
-#define NWC_STAGE_ENTRIES 1
-#endif
-// NWC_LADDER_PREFETCH: 1 = the ladder holds the next window's A/R entries in VGPRs through the
-// doublings (round 1-2 default); 0 = each entry is gathered coordinate by coordinate inside its
-// add (add_lt): no VGPR holds an entry across the doublings, the loop runs without spills, and
-// the sign of the digit is an address choice (+2.5 % verifies/s, profiles/r02/experiments.md).
-#ifndef NWC_LADDER_PREFETCH
-#define NWC_LADDER_PREFETCH 0
-#endif
-// NWC_LADDER_R_PREFETCH: 1 = in the uncached ladder the R entry's Y+X / Y-X are gathered inside
-// the A add, after the A entry's own loads (add_lt_pf), instead of at the start of the R add
-#ifndef NWC_LADDER_R_PREFETCH
-#define NWC_LADDER_R_PREFETCH 0
-#endif
-// cache policy of the basepoint-entry DMA (random rows of the 2.1 GB tables, used once): 0 =
-// default, 2 = non-temporal (A/B: keep L2/MALL for the per-lane tables)
-#ifndef NWC_BASE_FETCH_CPOL
-#define NWC_BASE_FETCH_CPOL 0
-#endif
-constexpr int STAGE_U4_PER_WAVE = NWC_STAGE_ENTRIES * 8 * 64;
+// One entry per stage: an 8 KB stage per wave; the second entry of a window is fetched after
+// the first one has been read (it lands during the first Niels add).  Measured +1.5 % verifies/s
+// over a 16 KB two-entry stage (5 interleaved A/B pairs on two boxes, profiles/r02/experiments.md),
+// at the same occupancy (VGPR-bound to 2 waves per SIMD); a non-temporal cache policy for the DMA
+// measured -0.9 % (profiles/r03/experiments.md).
+constexpr int STAGE_U4_PER_WAVE = 8 * 64;
 __device__ __forceinline__ void stage_fetch(uint4* stage, int e, const ge_niels_pad* src) {
   const uint4* g = reinterpret_cast<const uint4*>(src);
   _Pragma("unroll") for (int c = 0; c < 8; ++c)
-    __builtin_amdgcn_global_load_lds((nwc_gvoid*)(g + c), (nwc_lvoid*)(stage + (8 * e + c) * 64), 16, 0,
-                                     NWC_BASE_FETCH_CPOL);
+    __builtin_amdgcn_global_load_lds((nwc_gvoid*)(g + c), (nwc_lvoid*)(stage + (8 * e + c) * 64), 16, 0, 0);
 }
 __device__ __forceinline__ ge_niels stage_read(const uint4* stage, int e) {
   const int lane = threadIdx.x & 63;
@@ -895,10 +776,7 @@ __device__ __forceinline__ int base_fetch(int w, BaseDigits bd, i32& d0, i32& d1
     // for them below also has to wait for the DMA
     stage_wait();
     stage_fetch(stage, 0, T24 + (d0 < 0 ? -d0 : d0));
-    if (nb == 2) {
-      d1 = bd.p[(BD_HI + i) * 256];
-      if (NWC_STAGE_ENTRIES == 2) stage_fetch(stage, 1, T24 + B24_ENTRIES + (d1 < 0 ? -d1 : d1));
-    }
+    if (nb == 2) d1 = bd.p[(BD_HI + i) * 256];
   }
   return nb;
 }
@@ -909,13 +787,13 @@ __device__ __forceinline__ void base_adds(ge_p1p1& t, int nb, i32 d0, i32 d1, ui
 #pragma unroll 1
     for (int side = 0; side < nb; ++side) {
       const i32 dd_ = side ? d1 : d0;
-      const ge_niels e = stage_read(stage, NWC_STAGE_ENTRIES == 2 ? side : 0);
-      if (NWC_STAGE_ENTRIES == 1 && side + 1 < nb) {
+      const ge_niels e = stage_read(stage, 0);
+      if (side + 1 < nb) {
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): entry 0 is in VGPRs before the slot is reused
         stage_fetch(stage, 0, T24 + B24_ENTRIES + (d1 < 0 ? -d1 : d1));
       }
       t = ge_add_niels(ge_p1p1_to_p3_acc(t), ge_niels_cneg(e, dd_ < 0));
-      if (NWC_STAGE_ENTRIES == 1 && side + 1 < nb) stage_wait();
+      if (side + 1 < nb) stage_wait();
     }
   }
 }
@@ -925,69 +803,29 @@ __device__ __forceinline__ ge_p2 half_scalarmult(const LaneTable& ta, const Lane
                                                  uint4* stage, int W) {
   // Code-size discipline: the window body holds ONE doubling and ONE Niels add (rolled loops) and
   // two cached adds, so the hot loop stays inside the instruction cache.
-  // NWC_LADDER_PREFETCH=1 (round 1-2): the A/R entries of the next window are loaded at the end of
-  // the previous one, so their latency hides behind the doublings (80 VGPRs held through them).
   i32 da = cd.top, dr = dd.top;   // top digits are >= 0
-#if NWC_LADDER_PREFETCH
-  ge_cached ea = ta.load(da), er = tr.load(dr);
-  ge_p1p1 t = ge_cached_to_p1p1(lt_first(ta, da));
-#pragma unroll 1
-  for (int w = W - 1; w >= 0; --w) {
-    if (w != W - 1) ladder_dbl4(t);
-    i32 d0 = 0, d1 = 0;
-    const int nb = base_fetch(w, bd, d0, d1, T24, stage);
-    // two explicit adds (a rolled 2-iteration loop needs a selected copy of the entry: 40 more
-    // live VGPRs, which spilled)
-    if (w != W - 1) t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(ea, da < 0));
-    t = ge_add_cached(ge_p1p1_to_p3(t), ge_cached_cneg(er, dr < 0));
-    base_adds(t, nb, d0, d1, stage, T24);
-    if (w > 0) {
-      da = next16(cd);
-      dr = next16(dd);
-      ea = ta.load(da < 0 ? -da : da);
-      er = tr.load(dr < 0 ? -dr : dr);
-    }
-  }
-#else
-  // no entry held across the doublings: each is gathered inside its add; the digit strings are
-  // parked in LDS (BaseDigits), so the loop carries only the accumulator and a few scalars
+  // No entry is held across the doublings (holding the next window's entries through them, as
+  // rounds 1-2 did, kept 80 VGPRs live and spilled): each is gathered inside its add; the digit
+  // strings are parked in LDS (BaseDigits), so the loop carries only the accumulator and a few
+  // scalars
   park16(bd, BD_C, cd);
   park16(bd, BD_D, dd);
   ge_p1p1 t = ge_cached_to_p1p1(lt_first(ta, da));
 #pragma unroll 1
   for (int w = W - 1; w >= 0; --w) {
     i32 d0 = 0, d1 = 0;
-#if NWC_BASE_FETCH_EARLY
     // the window's first basepoint entry lands during the doublings; the A/R gathers issued
     // after it then never wait on the DMA (vmcnt counts in order)
     const int nb = base_fetch(w, bd, d0, d1, T24, stage);
-#endif
-#if NWC_LADDER_R_PREFETCH && NWC_PACKED_TABLES && NWC_BASE_FETCH_EARLY
-    if (w != W - 1) {
-      ladder_dbl4(t);
-      da = digit16(bd, BD_C, w, W);
-      dr = digit16(bd, BD_D, w, W);
-      uint4 rab[4];
-      t = add_lt_pf(t, ta, da < 0 ? -da : da, da < 0, tr, dr < 0 ? -dr : dr, dr < 0, rab);
-      t = add_lt_ab(t, rab, tr, dr < 0 ? -dr : dr, dr < 0);
-    } else {
-      t = add_lt(t, tr, dr < 0 ? -dr : dr, dr < 0);
-    }
-#else
     if (w != W - 1) {
       ladder_dbl4(t);
       da = digit16(bd, BD_C, w, W);
       t = add_lt(t, ta, da < 0 ? -da : da, da < 0);
       dr = digit16(bd, BD_D, w, W);
     }
-#if !NWC_BASE_FETCH_EARLY
-    const int nb = base_fetch(w, bd, d0, d1, T24, stage);
-#endif
     t = add_lt(t, tr, dr < 0 ? -dr : dr, dr < 0);
-#endif
     base_adds(t, nb, d0, d1, stage, T24);
   }
-#endif
   return ge_p1p1_to_p2(t);
 }
 
@@ -1181,67 +1019,6 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
     const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
     return ok && ident && h.ok;
   }
-#if NWC_PROLOGUE_LOOP
-  // Scalars first (challenge, lattice reduction, digit strings parked in LDS), then one rolled
-  // two-iteration loop decodes R and A in turn and writes each point's table at once: one point
-  // is live at a time, the decompression is inlined once (no call frame, no points passed through
-  // scratch memory), and nothing but the accumulator and two top digits reaches the ladder.
-  u32 sw[8];
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) sw[i] = sigw[8 + i];
-  bool ok = sc_lt_l(sw);
-  u32 kw[8];
-  challenge(sigw, aw, mw, kw);
-  const lat::HalfScalars h = lat::reduce(kw);
-  const int W = max(wave_windows(h.ok ? h.bits : 0), min(force_w, HALF_WINDOWS_MAX));
-  fallback = !h.ok;
-  {
-    Digits24 el, eh;
-    base_digits(h.d, sw, el, eh);
-    base_digits_park(bd, el, eh);
-  }
-  i32 c_top, d_top;
-  {
-    const Digits16 cd = recode16(h.c, W), dd = recode16(h.d, W);
-    park16(bd, BD_C, cd);
-    park16(bd, BD_D, dd);
-    c_top = cd.top;
-    d_top = dd.top;
-  }
-  const bool c_neg = h.c_neg;
-#pragma unroll 1
-  for (int j = 0; j < 2; ++j) {
-    // j = 0: R (table of -R);  j = 1: A (table of -c A / |c| = c < 0 ? A : -A)
-    u32 in[8];
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) in[i] = j ? aw[i] : sigw[i];
-    ge_p3 P;
-    u32 yc[8];
-    bool dok;
-    ge_decompress1(in, P, yc, dok);
-    const bool small = strict && ycanon_is_small_order(yc);
-    ok = ok && dok && !small;
-    const bool neg = (j == 0) || !c_neg;
-    P.X = fe_select(P.X, fe_neg(P.X), neg);
-    P.T = fe_select(P.T, fe_neg(P.T), neg);
-#if NWC_PROLOGUE_LOOP == 2
-    // park the point as its table's entry 1; both tables are built after the second decompression,
-    // right before the ladder reads them (a table written ~30k instructions earlier is colder)
-    LaneTable{j ? ta.p : tr.p}.store(1, ge_p3_to_cached(P));
-#else
-    build_table(LaneTable{j ? ta.p : tr.p}, P);
-#endif
-  }
-#if NWC_PROLOGUE_LOOP == 2
-#pragma unroll 1
-  for (int j = 0; j < 2; ++j) {
-    const LaneTable tab{j ? ta.p : tr.p};
-    const ge_p3 P = ge_p1p1_to_p3(ge_cached_to_p1p1(lt_first(tab, 1)));
-    build_table(tab, P);
-  }
-#endif
-  const ge_p2 q = half_scalarmult_parked(ta, tr, c_top, d_top, bd, T24, stage, W);
-  const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
-  return ok && ident && h.ok;
-#else
   Prologue p;
   prologue<1>(p, mw, aw, sigw, strict);
   const lat::HalfScalars h = lat::reduce(p.kw);
@@ -1259,7 +1036,6 @@ __device__ __forceinline__ bool verify_half(const u32 mw[8], const u32 aw[8], co
   const ge_p2 q = half_scalarmult(ta, tr, cd, dd, bd, T24, stage, W);
   const bool ident = fe_is_zero(q.X) && fe_is_zero(fe_sub(q.Y, q.Z));
   return p.ok && ident && h.ok;
-#endif
 }
 
 // ------------------------------------------------------------------------------- verify
@@ -1830,12 +1606,6 @@ __device__ gs_p2 gs_mul_bits(const gs_p3& P, const u32 m[8], int hi, int lo) {
   }
   return acc;
 }
-#ifndef NWC_COLD_BSUM_WAVE0
-#define NWC_COLD_BSUM_WAVE0 0
-#endif
-#ifndef NWC_COLD_TIMING
-#define NWC_COLD_TIMING 0   // 1: block 0 prints per-wave phase times (A/B builds only)
-#endif
 // [e] B from the radix-2^22 basepoint comb (COMB16_WINDOWS entries, one addition each), cached
 __device__ gs_cached cold_comb_sum(const ge_niels_pad* comb16, const u32 e[8]) {
   u32 sd[9];
@@ -1865,14 +1635,7 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
   const bool leaf = a.strict == 0;
   if (threadIdx.x == 0) sh.ready = 0;
   __syncthreads();
-#if NWC_COLD_TIMING
-  const uint64_t ct0 = wall_clock64();
-  __shared__ uint32_t ctv[4][4];
-  int ctn = 0;
-#define CT(tag) do { if (lane == 0) ctv[wave][ctn] = (uint32_t)(wall_clock64() - ct0); ++ctn; } while (0)
-#else
 #define CT(tag) do {} while (0)
-#endif
   u32 mw[8], aw[8], sgw[16];
   load_inputs(a, i, mw, aw, sgw);
   u32 rw[8], sw[8];
@@ -1888,14 +1651,12 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
       if (lane < 10) { sh.tu[0][lane] = U.v; sh.tu[1][lane] = W.v; }
     }
     CT("xonly");
-#if !NWC_COLD_BSUM_WAVE0
     // then [d s mod l] B from the radix-2^22 basepoint comb: 12 entries, 11 additions, no
     // doublings (wave 0 has published the scalar by now in a batch leaf; a strict call waits here)
     while (__hip_atomic_load(&sh.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 3) __builtin_amdgcn_s_sleep(1);
     u32 eb[8];
     _Pragma("unroll") for (int q = 0; q < 8; ++q) eb[q] = sh.bs[q];
     cold_store(sh.bsum, cold_comb_sum(comb16, eb));
-#endif
     CT("bsum");
     __syncthreads();
     return;
@@ -1913,9 +1674,6 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
       sh.cd = cd; sh.dd = dd;
       _Pragma("unroll") for (int q = 0; q < 8; ++q) sh.bs[q] = eb[q];
     }
-#if NWC_COLD_BSUM_WAVE0
-    cold_store(sh.bsum, cold_comb_sum(comb16, eb));   // A/B: the comb sum in wave 0's phase 1
-#endif
   } else {
     fe X, Y;
     u32 yc[8];
@@ -2006,11 +1764,6 @@ __global__ __launch_bounds__(256) void k_verify_cold(VerifyArgs a, const ge_niel
   t = gs_add_cached(gs_to_p3(t), cold_load(sh.bsum, false));
   const bool ident = gs_is_identity(gs_to_p2(t));
   CT("final");
-#if NWC_COLD_TIMING
-  if (blockIdx.x == 0 && lane == 0)
-    printf("cold ticks w0 %u %u | w1 %u %u %u | w2 %u %u | w3 %u %u\n", ctv[0][0], ctv[0][1], ctv[1][0], ctv[1][1],
-           ctv[1][2], ctv[2][0], ctv[2][1], ctv[3][0], ctv[3][1]);
-#endif
   bool torsion = false;
   if (leaf) {
     // u([l - 2^252] A) = (Z + Y : Z - Y);  same u  <=>  U (Z - Y) = W (Z + Y)

@@ -147,6 +147,7 @@ struct DevCtx {
   nwc::ge_niels_pad* cm_comb = nullptr;   // per-key combs (committees of <= COMB_MAX_KEYS keys)
   int32_t* cm_slots = nullptr;
   uint32_t cm_n = 0, cm_slot_mask = 0;
+  size_t cm_bytes = 0;                  // device bytes of the committee cache (nwc_memory_info)
   uint8_t* arena = nullptr;
   size_t arena_cap = 0;
   // config::Committee stake / worker tables (nwc_set_committee_config)
@@ -254,6 +255,22 @@ struct Carve {
 uint32_t auto_keys_cap();
 int auto_grow(DevCtx& d, uint32_t ncap);
 bool comb16_enabled();
+
+// Test and A/B knobs settable at run time (nwc_diag_set), defaults from the environment read once:
+// NWC_STRAUS_NQ (votes per Straus sub-batch, 12) and NWC_FORCE_WINDOWS (half-ladder window count
+// forced on every wave, 0 = off).  Atomics: a setter racing a launch gives that launch either value.
+struct Knobs {
+  std::atomic<uint32_t> straus_nq{12};
+  std::atomic<uint32_t> force_windows{0};
+  Knobs() {
+    if (const char* e = std::getenv("NWC_STRAUS_NQ")) straus_nq = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("NWC_FORCE_WINDOWS")) force_windows = (uint32_t)std::strtoul(e, nullptr, 10);
+  }
+};
+Knobs& knobs() {
+  static Knobs k;
+  return k;
+}
 
 int init_device(DevCtx& d) {
   HIP_TRY(hipSetDevice(d.hip_id));
@@ -681,7 +698,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
   nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
-  if (const char* e = std::getenv("NWC_FORCE_WINDOWS")) a.force_windows = (uint32_t)std::strtoul(e, nullptr, 10);
+  a.force_windows = knobs().force_windows.load();
   const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
   const bool half = path != VPath::Full;
   // small batch-leaf launches outside the comb path: the keys' torsion test (one long serial
@@ -1003,9 +1020,8 @@ int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8
   if (nvotes > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "more than 2^32 - 1 votes in one call");
   if (!d.comb16)   // no basepoint comb (NWC_COMB16=0): the exact leaves
     return launch_verify(d, dig, mi, 0, pks, sigs, nvotes, 0, leaf, s);
-  // sub-batches of ~NWC_STRAUS_NQ votes (default 12), every lane slot the same number of rounds
-  uint32_t target = 12;
-  if (const char* e = std::getenv("NWC_STRAUS_NQ")) target = (uint32_t)std::strtoul(e, nullptr, 10);   // A/B
+  // sub-batches of ~12 votes (knobs().straus_nq), every lane slot the same number of rounds
+  const uint32_t target = knobs().straus_nq.load();
   const uint64_t resident = (uint64_t)d.cus * nwc::STRAUS_WAVES_PER_SIMD * 256;
   const uint64_t runs = nwc::straus_runs(nvotes, resident, target);
   const uint64_t lanes = std::min<uint64_t>((runs + 255) / 256 * 256, resident);
@@ -1127,7 +1143,31 @@ int nwc_cert_cuts(const uint32_t* offsets, size_t m, uint32_t world, uint64_t* c
   return 0;
 }
 
-int nwc_version(void) { return (1 << 16) | 0; }
+int nwc_version(void) { return (1 << 16) | 1; }
+
+#ifndef NWC_BUILD_ID
+#define NWC_BUILD_ID "unknown"
+#endif
+// "NWC_BUILD_ID:" + the hash narwhal_amd/build.py takes over the sources and flags; build.py finds
+// it in the .so's bytes to decide whether the library is HEAD's.
+static const char k_build_id[] = "NWC_BUILD_ID:" NWC_BUILD_ID;
+const char* nwc_build_id(void) { return k_build_id + 13; }
+
+int nwc_diag_set(const char* name, int64_t value) {
+  if (!name) return set_err(NWC_ERR_ARG, "null knob name");
+  if (value < 0 || value > 0xFFFFFFFFll) return set_err(NWC_ERR_ARG, "knob value out of range");
+  if (std::strcmp(name, "straus_nq") == 0) {
+    if (value < 1 || value > nwc::STRAUS_MAX_PER_LANE) return set_err(NWC_ERR_ARG, "straus_nq must be in [1, %d]", nwc::STRAUS_MAX_PER_LANE);
+    knobs().straus_nq = (uint32_t)value;
+  } else if (std::strcmp(name, "force_windows") == 0) {
+    if (value != 0 && (value < nwc::HALF_WINDOWS_MIN || value > nwc::HALF_WINDOWS_MAX))
+      return set_err(NWC_ERR_ARG, "force_windows must be 0 or in [%d, %d]", nwc::HALF_WINDOWS_MIN, nwc::HALF_WINDOWS_MAX);
+    knobs().force_windows = (uint32_t)value;
+  } else {
+    return set_err(NWC_ERR_ARG, "unknown knob '%s'", name);
+  }
+  return 0;
+}
 
 const char* nwc_last_error(void) { return t_err.c_str(); }
 
@@ -1362,7 +1402,7 @@ static int set_committee_locked(const uint8_t* pks, size_t n) {
     if (d.cc_worker_off) HIP_TRY(hipFree(d.cc_worker_off));
     if (d.cc_worker_ids) HIP_TRY(hipFree(d.cc_worker_ids));
     d.cc_stakes = nullptr; d.cc_worker_off = nullptr; d.cc_worker_ids = nullptr; d.cc_n = 0;
-    d.cm_n = 0; d.cm_slot_mask = 0;
+    d.cm_n = 0; d.cm_slot_mask = 0; d.cm_bytes = 0;
     if (n == 0) continue;
     HIP_TRY(hipMalloc(&d.cm_keys, 32 * n));
     HIP_TRY(hipMalloc(&d.cm_flags, 4 * n));
@@ -1383,6 +1423,8 @@ static int set_committee_locked(const uint8_t* pks, size_t n) {
     HIP_TRY(hipStreamSynchronize(d.stream));
     d.cm_n = (uint32_t)n;
     d.cm_slot_mask = slots - 1;
+    d.cm_bytes = 36 * n + n * 129 * sizeof(nwc::ge_niels) + 4 * (size_t)slots +
+                 (d.cm_comb ? n * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad) : 0);
   }
   if (n) {
     std::lock_guard<std::mutex> lk(g_hcm.mu);
@@ -1757,3 +1799,55 @@ int nwc_dev_sanitize_messages(const void* d_data, const void* d_offsets, uint64_
 }  // extern "C"
 
 #include "digester.h"
+
+extern "C" {
+
+int nwc_memory_info(nwc_memory* out) {
+  if (int rc = require_init()) return rc;
+  if (!out) return set_err(NWC_ERR_ARG, "null argument");
+  DevCtx* dp = ctx(t_dev);
+  if (!dp) return set_err(NWC_ERR_ARG, "device index %d not initialised", t_dev);
+  DevCtx& d = *dp;
+  *out = nwc_memory{};
+  {
+    std::lock_guard<std::mutex> lk(d.mu);
+    out->tables = 2 * 129 * sizeof(nwc::ge_niels) + 2 * (size_t)nwc::B24_ENTRIES * sizeof(nwc::ge_niels_pad) +
+                  2 * sizeof(nwc::ge_p3) + nwc::BaseComb::per * sizeof(nwc::ge_niels_pad) +
+                  (d.comb16 ? nwc::COMB16_TOTAL * sizeof(nwc::ge_niels_pad) + nwc::COMB16_WINDOWS * sizeof(nwc::ge_p3) : 0) +
+                  36 * (size_t)NWC_MEMO_SLOTS;
+    out->committee = d.cm_bytes;
+    out->auto_cache = (size_t)d.ak_cap * (36 + 129 * sizeof(nwc::ge_niels) + nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad)) +
+                      4 * (size_t)d.ak_slot_cap + d.kb_cap * sizeof(nwc::ge_p3);
+    out->scratch = d.scratch_cap + d.straus_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap +
+                   8 * (size_t)d.ts_slot_count;
+  }
+  out->digesters = digester_device_bytes(d.hip_id);
+  size_t fr = 0, tot = 0;
+  HIP_TRY(hipSetDevice(d.hip_id));
+  HIP_TRY(hipMemGetInfo(&fr, &tot));
+  out->device_free = fr;
+  out->device_total = tot;
+  return 0;
+}
+
+int nwc_trim(void) {
+  if (int rc = require_init()) return rc;
+  DevCtx* dp = ctx(t_dev);
+  if (!dp) return set_err(NWC_ERR_ARG, "device index %d not initialised", t_dev);
+  DevCtx& d = *dp;
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  // every stream: nwc_dev_* launches on callers' streams read these buffers too
+  HIP_TRY(hipDeviceSynchronize());
+  if (d.scratch) HIP_TRY(hipFree(d.scratch));
+  if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
+  if (d.arena) HIP_TRY(hipFree(d.arena));
+  if (d.msg_arena) HIP_TRY(hipFree(d.msg_arena));
+  d.scratch = nullptr; d.scratch_cap = 0;
+  d.straus_scratch = nullptr; d.straus_cap = 0;
+  d.arena = nullptr; d.arena_cap = 0;
+  d.msg_arena = nullptr; d.msg_arena_cap = 0;
+  return 0;
+}
+
+}  // extern "C"

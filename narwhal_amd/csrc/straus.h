@@ -29,17 +29,8 @@
 
 namespace nwc {
 
-#ifndef NWC_STRAUS_FULL_PREFETCH
-#define NWC_STRAUS_FULL_PREFETCH 1
-#endif
-#ifndef NWC_STRAUS_PREFETCH2
-#define NWC_STRAUS_PREFETCH2 0
-#endif
 #ifndef NWC_STRAUS_WAVES_PER_SIMD
 #define NWC_STRAUS_WAVES_PER_SIMD 2
-#endif
-#ifndef NWC_STRAUS_VOTE_MAJOR
-#define NWC_STRAUS_VOTE_MAJOR 0
 #endif
 constexpr int STRAUS_WAVES_PER_SIMD = NWC_STRAUS_WAVES_PER_SIMD;
 constexpr int STRAUS_MAX_PER_LANE = 16;
@@ -128,14 +119,10 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
   __shared__ u32 dl[STRAUS_LDS_WORDS];
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
-  // vote t of lane slot l: vote-major ([t][l], a wave's 64 lanes of one vote within 156 KB, as the
-  // leaf kernel's tables) or lane-major ([l][t], a wave's gather spread over 64 x lane_stride)
-#if NWC_STRAUS_VOTE_MAJOR
-  auto vote_base = [&](uint64_t t) { return a.scratch + (t * lanes + slot) * STRAUS_VOTE_BYTES; };
-#else
+  // vote t of lane slot l, lane-major ([l][t]; a vote-major layout measured no better,
+  // profiles/r03/experiments.md)
   uint8_t* const base = a.scratch + slot * a.lane_stride;
   auto vote_base = [&](uint64_t t) { return base + t * STRAUS_VOTE_BYTES; };
-#endif
   // entry 0 (the identity) of the first vote's tables: the add every lane of a wave makes in a
   // (window, vote) step where it has no vote of its own reads it
   LaneTable{reinterpret_cast<uint4*>(vote_base(0))}.store(0, ge_cached_identity());
@@ -219,31 +206,6 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
         tab = LaneTable{reinterpret_cast<uint4*>(vote_base(u < nq ? u : 0) + kind * TAB_BYTES_PER_LANE)};
         d = (i32)((dl[(2 * u + kind) * 256 + threadIdx.x] >> sh) & 15u) - 8;
       };
-#if NWC_PACKED_TABLES
-#if NWC_STRAUS_FULL_PREFETCH && NWC_STRAUS_PREFETCH2
-      // two additions ahead: the entry an add consumes was gathered ~2.9k instructions earlier
-      i32 d0, d1 = 0;
-      LaneTable tq;
-      entry(0, d0, tq);
-      uint4 q0[8], q1[8];
-      lt_load_full(tq, d0 < 0 ? -d0 : d0, d0 < 0, q0);
-      if (nadd > 1) {
-        entry(1, d1, tq);
-        lt_load_full(tq, d1 < 0 ? -d1 : d1, d1 < 0, q1);
-      }
-#pragma unroll 1
-      for (uint32_t j = 0; j < nadd; ++j) {
-        const bool neg = d0 < 0;
-        uint4 cur[8];
-        _Pragma("unroll") for (int k = 0; k < 8; ++k) { cur[k] = q0[k]; q0[k] = q1[k]; }
-        d0 = d1;
-        if (j + 2 < nadd) {
-          entry(j + 2, d1, tq);
-          lt_load_full(tq, d1 < 0 ? -d1 : d1, d1 < 0, q1);
-        }
-        t = add_lt_full(t, cur, neg);
-      }
-#elif NWC_STRAUS_FULL_PREFETCH
       i32 dn;
       LaneTable tn;
       entry(0, dn, tn);
@@ -260,33 +222,6 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
         }
         t = add_lt_full(t, cur, neg);
       }
-#else
-      i32 dn;
-      LaneTable tn;
-      entry(0, dn, tn);
-      uint4 ab[4];
-      lt_load_ab(tn, dn < 0 ? -dn : dn, dn < 0, ab);
-#pragma unroll 1
-      for (uint32_t j = 0; j < nadd; ++j) {
-        const i32 d = dn;
-        const LaneTable tab = tn;
-        uint4 cur[4] = {ab[0], ab[1], ab[2], ab[3]};
-        if (j + 1 < nadd) {
-          entry(j + 1, dn, tn);
-          lt_load_ab(tn, dn < 0 ? -dn : dn, dn < 0, ab);
-        }
-        t = add_lt_ab(t, cur, tab, d < 0 ? -d : d, d < 0);
-      }
-#endif
-#else
-#pragma unroll 1
-      for (uint32_t j = 0; j < nadd; ++j) {
-        i32 d;
-        LaneTable tab;
-        entry(j, d, tab);
-        t = add_lt(t, tab, d < 0 ? -d : d, d < 0);
-      }
-#endif
     }
     // ---- phase 3: + (-S) B from the basepoint comb, identity test
     ge_p3 P = ge_p1p1_to_p3(t);

@@ -35,6 +35,15 @@ def worker_primary_message(digest: bytes, worker_id: int, own_digest: bool) -> b
     return struct.pack("<I", OUR_BATCH if own_digest else OTHERS_BATCH) + digest + struct.pack("<I", worker_id)
 
 
+class DigestGroupError(_lib.DeviceError):
+    """A group of batches failed on the device (nwc_digester_poll < 0): `tags` are the batches it
+    held, handed back so the caller can release or retry them."""
+
+    def __init__(self, msg: str, tags: List[int]):
+        super().__init__(msg)
+        self.tags = tags
+
+
 class Digester:
     """ctypes handle of one `nwc_digester` (its drain thread runs inside libnwc).  Keeps every
     submitted batch alive until its digest has been polled (the C side borrows it)."""
@@ -50,15 +59,20 @@ class Digester:
         self._lock = threading.Lock()
 
     def submit(self, batch, tag: Optional[int] = None) -> int:
-        """Queue one batch (bytes-like); returns its tag (a sequence number unless given)."""
-        buf = _lib.buf(batch)
+        """Queue one batch (bytes, bytearray or a C-contiguous uint8 numpy array); returns its tag
+        (a sequence number unless given).  The batch is held until its digest has been polled."""
+        buf = _lib.buf(batch)   # TypeError for other types and for non-contiguous arrays
         n = batch.nbytes if hasattr(batch, "nbytes") else len(batch)
         with self._lock:
             if tag is None:
                 tag = self._next
             self._next = max(self._next, tag + 1)
             self._held[tag] = (batch, buf)
-        _lib.check(self.lib.nwc_digester_submit(self.h, buf, n, tag))
+        rc = self.lib.nwc_digester_submit(self.h, buf, n, tag)
+        if rc < 0:
+            with self._lock:
+                self._held.pop(tag, None)   # not queued: the C side does not borrow it
+            _lib.check(rc)
         return tag
 
     def arena(self, nbytes: int):
@@ -87,7 +101,10 @@ class Digester:
         with self._lock:
             for t, _ in out:
                 self._held.pop(t, None)
-        _lib.check(rc)
+        if rc < 0:
+            # a failed group's tags (no digests), or the sticky error once nothing is left
+            raise DigestGroupError("libnwc error %d: %s" % (rc, self.lib.nwc_last_error().decode()),
+                                   [t for t, _ in out])
         return out
 
     def stats(self) -> Tuple[int, int, int]:
@@ -112,6 +129,7 @@ class Processor:
         # always digests on the GPU (a missing libnwc raises here)
         self.dg = digester if digester is not None else Digester(max_group, max_wait_us)
         self._pending: Dict[int, bytes] = {}
+        self._next_tag = 0
         self._submitted = 0
         self._done = 0
         self._closed = threading.Event()
@@ -127,34 +145,45 @@ class Processor:
 
     def _feed(self):
         try:
-            while True:
+            while self._error is None:
                 batch = self.rx.get()
                 if batch is None:   # channel closed
                     break
-                tag = self._submitted
+                tag = self._next_tag
                 self._pending[tag] = batch
-                self._submitted += 1
-                self.dg.submit(batch, tag)
+                try:
+                    self.dg.submit(batch, tag)
+                except BaseException:
+                    self._pending.pop(tag, None)
+                    raise
+                self._next_tag += 1
+                self._submitted += 1   # counted only once the digester holds it
         except BaseException as e:  # noqa: BLE001 (reported by join())
-            self._error = e
+            self._error = self._error or e
         finally:
             self._closed.set()
 
     def _collect(self):
         try:
-            while not (self._closed.is_set() and self._done == self._submitted):
+            # stops on the feeder's error too: batches it never submitted will not come back
+            while self._error is None and not (self._closed.is_set() and self._done == self._submitted):
                 for tag, digest in self.dg.poll(4096, 2000):
                     batch = self._pending.pop(tag)
                     self.store.write(digest, batch)                                   # :41
                     self.tx.put(worker_primary_message(digest, self.id, self.own))    # :44-53
                     self._done += 1
         except BaseException as e:  # noqa: BLE001
-            self._error = e
+            self._error = self._error or e
 
     def join(self, timeout: Optional[float] = None) -> None:
-        """Wait until the closed channel's last batch has been stored and sent; frees the digester."""
+        """Wait until the closed channel's last batch has been stored and sent; frees the digester.
+        Raises TimeoutError (and keeps the digester) if the threads are still running after
+        `timeout`, and the first error of either thread otherwise."""
         self._feeder.join(timeout)
         self._collector.join(timeout)
+        if self._feeder.is_alive() or self._collector.is_alive():
+            # never free the digester under a thread that may be inside poll or submit
+            raise TimeoutError("Processor still running after %.1f s" % timeout)
         self.dg.close()
         if self._error:
             raise self._error

@@ -7,6 +7,20 @@ use std::os::raw::{c_char, c_int, c_void};
 #[allow(non_camel_case_types)]
 pub enum nwc_digester {}
 
+/// Device bytes this process holds on one device (nwc_memory_info).
+#[allow(non_camel_case_types)]
+#[repr(C)]
+#[derive(Default, Debug, Clone, Copy)]
+pub struct nwc_memory {
+    pub tables: u64,
+    pub committee: u64,
+    pub auto_cache: u64,
+    pub scratch: u64,
+    pub digesters: u64,
+    pub device_free: u64,
+    pub device_total: u64,
+}
+
 #[link(name = "nwc")]
 extern "C" {
     pub fn nwc_init(device_mask: u32) -> c_int;
@@ -14,6 +28,10 @@ extern "C" {
     pub fn nwc_last_error() -> *const c_char;
     pub fn nwc_version() -> c_int;
     pub fn nwc_device_count() -> c_int;
+    pub fn nwc_build_id() -> *const c_char;
+    pub fn nwc_memory_info(out: *mut nwc_memory) -> c_int;
+    pub fn nwc_trim() -> c_int;
+    pub fn nwc_diag_set(name: *const c_char, value: i64) -> c_int;
 
     pub fn nwc_verify_strict(msg32: *const u8, pk: *const u8, sig: *const u8) -> c_int;
     pub fn nwc_verify_batch(msg32: *const u8, pks: *const u8, sigs: *const u8, n: usize, bad_bitmap: *mut u8) -> c_int;

@@ -139,18 +139,22 @@ impl BatchDigester {
     }
 
     /// The oldest outstanding batch with its digest, waiting up to `wait_us` (None on timeout).
-    pub fn next(&mut self, wait_us: u32) -> Option<([u8; 32], Vec<u8>)> {
+    /// A batch whose group failed on the device comes back as `Err(batch)` -- the caller keeps
+    /// it (to hash on the CPU, retry or drop) -- so `held` and the returned tags never diverge;
+    /// the library's sticky error with nothing left to return panics like every device error.
+    pub fn next(&mut self, wait_us: u32) -> Option<Result<([u8; 32], Vec<u8>), Vec<u8>>> {
         if self.held.is_empty() {
             return None;
         }
         let (mut tag, mut dig, mut n) = (0u64, [0u8; 32], 0usize);
-        check(unsafe { ffi::nwc_digester_poll(self.q, 1, wait_us, &mut tag, dig.as_mut_ptr(), &mut n) });
+        let rc = unsafe { ffi::nwc_digester_poll(self.q, 1, wait_us, &mut tag, dig.as_mut_ptr(), &mut n) };
         if n == 0 {
+            check(rc);
             return None;
         }
         let (t, batch) = self.held.pop_front().unwrap();
         assert_eq!(t, tag, "digests come back in submission order");
-        Some((dig, batch))
+        Some(if rc < 0 { Err(batch) } else { Ok((dig, batch)) })
     }
 }
 

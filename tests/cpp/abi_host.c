@@ -16,6 +16,21 @@
  *                                       -> "L <rc> <first> <second> <p50> <p90> <p99> <p99.9> <max> <mean>"
  *                                          per-call latency (us) of nwc_verify_batch timed in C;
  *                                          percentiles over calls warm..calls-1
+ *   T <m> <offsets m+1>, votes and digests as C -> "T <rc> <cert bitmap> <bad bitmap>"
+ *                                          (nwc_verify_batch_straus_many)
+ *   Q <n>, then n lines <pk32 stake nworkers wid...>  -> "Q <rc>"  (nwc_set_committee_config)
+ *   M <m> <gc_round> <target72 | ->, then m lines <msg hex> -> "M <rc> <code,kind,digest32>..."
+ *                                          (nwc_sanitize_messages)
+ *   G <max_group> <wait_us> <arena 0/1> <n>, then n lines <data hex | ->
+ *                                       -> per result "g <tag> <digest32>" or "g <tag> ERR <rc>",
+ *                                          then "G <destroy rc>": a digester fed every batch (from
+ *                                          malloc'd buffers, or written into its receive arena),
+ *                                          polled until every tag is back; the batches and their
+ *                                          digests are kept for Y
+ *   Y <verify threads> <rounds>         -> "Y <mismatches>": one thread streams the last G's
+ *                                          batches through a new digester `rounds` times while
+ *                                          the verify threads re-run every B request and the
+ *                                          last V request on the same device
  *   Z                                   -> a heap read one byte out of bounds (sanitizer self-check)
  * Built by __graft_entry__.build() into tests/cpp/build/abi_host (and, host code under
  * AddressSanitizer + UBSan against a sanitized libnwc, abi_host_asan); run by
@@ -47,6 +62,14 @@ typedef struct {
 static breq g_b[4096];
 static size_t g_nb;
 static int g_rounds;
+/* the last V request (re-run by Y) */
+static unsigned char *g_vm, *g_vp, *g_vs, *g_vbits;
+static size_t g_vn;
+/* the last G command's batches and digests (streamed again by Y) */
+static unsigned char** g_gb;
+static size_t* g_glen;
+static unsigned char* g_gdig;
+static size_t g_gn;
 
 static void* worker(void* arg) {
   long bad_count = 0;
@@ -61,6 +84,46 @@ static void* worker(void* arg) {
     }
   }
   return (void*)bad_count;
+}
+
+/* Y: one digester streaming the G batches `g_rounds` times, compared with the G digests */
+static void* digest_streamer(void* arg) {
+  long mism = 0;
+  (void)arg;
+  nwc_digester* q = nwc_digester_create(64, 500);
+  if (!q) return (void*)1000000L;
+  uint64_t* tags = malloc(sizeof(uint64_t) * (g_gn + 1));
+  unsigned char* dig = malloc(32 * (g_gn + 1));
+  for (int r = 0; r < g_rounds; ++r) {
+    for (size_t i = 0; i < g_gn; ++i)
+      if (nwc_digester_submit(q, g_gb[i], g_glen[i], (uint64_t)r * g_gn + i) != 0) ++mism;
+    size_t got = 0;
+    while (got < g_gn) {
+      size_t n = 0;
+      if (nwc_digester_poll(q, g_gn - got, 200000, tags, dig, &n) != 0) { ++mism; break; }
+      for (size_t k = 0; k < n; ++k) {
+        const uint64_t want = (uint64_t)r * g_gn + got + k;
+        if (tags[k] != want || memcmp(dig + 32 * k, g_gdig + 32 * (want - (uint64_t)r * g_gn), 32) != 0) ++mism;
+      }
+      got += n;
+    }
+  }
+  if (nwc_digester_destroy(q) != 0) ++mism;
+  free(tags);
+  free(dig);
+  return (void*)mism;
+}
+
+/* Y: the B requests and the last V request, re-run */
+static void* verifier(void* arg) {
+  long mism = (long)(size_t)worker(arg);
+  for (int r = 0; r < g_rounds && g_vn; ++r) {
+    unsigned char* bits = calloc(g_vn / 8 + 1, 1);
+    if (nwc_verify_strict_many(g_vm, g_vp, g_vs, g_vn, bits) != 0 || memcmp(bits, g_vbits, (g_vn + 7) / 8) != 0)
+      ++mism;
+    free(bits);
+  }
+  return (void*)mism;
 }
 
 static int unhex(const char* s, unsigned char* out, size_t n) {
@@ -145,11 +208,17 @@ int main(void) {
       printf("V %d ", rc);
       puthex(bits, (n + 7) / 8);
       printf("\n");
-      free(ms);
-      free(pks);
-      free(sigs);
-      free(bits);
-    } else if (tok[0] == 'C') {
+      free(g_vm);
+      free(g_vp);
+      free(g_vs);
+      free(g_vbits);
+      g_vm = ms;
+      g_vp = pks;
+      g_vs = sigs;
+      g_vbits = bits;
+      g_vn = rc == 0 ? n : 0;
+    } else if (tok[0] == 'C' || tok[0] == 'T') {
+      const char kind = tok[0];
       const char* cnt = strtok(NULL, " \n");
       if (!cnt) return 3;
       const size_t mc = (size_t)strtoul(cnt, NULL, 10);
@@ -176,8 +245,9 @@ int main(void) {
       }
       unsigned char* cert = calloc(mc / 8 + 1, 1);
       unsigned char* badv = calloc(nv / 8 + 1, 1);
-      rc = nwc_verify_batch_many(dig, offs, pks, sigs, mc, cert, badv);
-      printf("C %d ", rc);
+      rc = kind == 'C' ? nwc_verify_batch_many(dig, offs, pks, sigs, mc, cert, badv)
+                       : nwc_verify_batch_straus_many(dig, offs, pks, sigs, mc, cert, badv);
+      printf("%c %d ", kind, rc);
       puthex(cert, (mc + 7) / 8);
       printf(" ");
       puthex(badv, (nv + 7) / 8);
@@ -256,6 +326,175 @@ int main(void) {
       free(us);
       free(pks);
       free(sigs);
+    } else if (tok[0] == 'Q') {
+      /* Q n, then n lines "pk stake nworkers wid...": nwc_set_committee_config */
+      const char* cnt = strtok(NULL, " \n");
+      if (!cnt) return 3;
+      const size_t n = (size_t)strtoul(cnt, NULL, 10);
+      unsigned char* pks = malloc(32 * n + 1);
+      uint64_t* stakes = malloc(8 * n + 8);
+      uint32_t* woff = malloc(4 * (n + 1));
+      uint32_t* wids = malloc(4 * (8 * n + 1));
+      woff[0] = 0;
+      for (size_t i = 0; i < n; ++i) {
+        if (!fgets(line, sizeof line, stdin)) return 3;
+        const char* p = strtok(line, " \n");
+        const char* st = strtok(NULL, " \n");
+        const char* nw = strtok(NULL, " \n");
+        if (!p || !st || !nw || unhex(p, pks + 32 * i, 32)) return 3;
+        stakes[i] = strtoull(st, NULL, 10);
+        const unsigned k = (unsigned)strtoul(nw, NULL, 10);
+        if (k > 8) return 3;
+        woff[i + 1] = woff[i] + k;
+        for (unsigned j = 0; j < k; ++j) {
+          const char* w = strtok(NULL, " \n");
+          if (!w) return 3;
+          wids[woff[i] + j] = (uint32_t)strtoul(w, NULL, 10);
+        }
+      }
+      printf("Q %d\n", nwc_set_committee_config(pks, stakes, n, woff, wids));
+      free(pks);
+      free(stakes);
+      free(woff);
+      free(wids);
+    } else if (tok[0] == 'M') {
+      /* M m gc_round target|-, then m message lines: nwc_sanitize_messages */
+      const char* cnt = strtok(NULL, " \n");
+      const char* gc = strtok(NULL, " \n");
+      const char* tg = strtok(NULL, " \n");
+      if (!cnt || !gc || !tg) return 3;
+      const size_t m = (size_t)strtoul(cnt, NULL, 10);
+      unsigned char target[72];
+      const int has_target = strcmp(tg, "-") != 0;
+      if (has_target && unhex(tg, target, 72)) return 3;
+      unsigned char** msg = malloc(sizeof(unsigned char*) * (m + 1));
+      size_t* len = malloc(sizeof(size_t) * (m + 1));
+      size_t total = 0;
+      for (size_t i = 0; i < m; ++i) {
+        if (!fgets(line, sizeof line, stdin)) return 3;
+        const char* h = strtok(line, " \n");
+        len[i] = (h && strcmp(h, "-") != 0) ? strlen(h) / 2 : 0;
+        msg[i] = malloc(len[i] + 1);
+        if (len[i] && unhex(h, msg[i], len[i])) return 3;
+        total += len[i];
+      }
+      unsigned char* data = malloc(total + 1);
+      uint64_t* offs = malloc(8 * (m + 1));
+      offs[0] = 0;
+      for (size_t i = 0; i < m; ++i) {
+        memcpy(data + offs[i], msg[i], len[i]);
+        offs[i + 1] = offs[i] + len[i];
+        free(msg[i]);
+      }
+      int32_t* codes = malloc(4 * (m + 1));
+      unsigned char* digs = malloc(32 * (m + 1));
+      unsigned char* kinds = malloc(m + 1);
+      rc = nwc_sanitize_messages(data, offs, m, strtoull(gc, NULL, 10), has_target ? target : NULL, codes, digs, kinds);
+      printf("M %d", rc);
+      for (size_t i = 0; rc == 0 && i < m; ++i) {
+        printf(" %d,%d,", codes[i], kinds[i]);
+        puthex(digs + 32 * i, 32);
+      }
+      printf("\n");
+      free(msg);
+      free(len);
+      free(data);
+      free(offs);
+      free(codes);
+      free(digs);
+      free(kinds);
+    } else if (tok[0] == 'G') {
+      /* G max_group wait_us arena n, then n data lines: the worker digester end to end */
+      const char* a1 = strtok(NULL, " \n");
+      const char* a2 = strtok(NULL, " \n");
+      const char* a3 = strtok(NULL, " \n");
+      const char* a4 = strtok(NULL, " \n");
+      if (!a1 || !a2 || !a3 || !a4) return 3;
+      const uint32_t max_group = (uint32_t)strtoul(a1, NULL, 10), wait_us = (uint32_t)strtoul(a2, NULL, 10);
+      const int use_arena = atoi(a3);
+      const size_t n = (size_t)strtoul(a4, NULL, 10);
+      for (size_t i = 0; i < g_gn; ++i) free(g_gb[i]);
+      free(g_gb);
+      free(g_glen);
+      free(g_gdig);
+      g_gb = malloc(sizeof(unsigned char*) * (n + 1));
+      g_glen = malloc(sizeof(size_t) * (n + 1));
+      g_gdig = calloc(32 * (n + 1), 1);
+      g_gn = n;
+      size_t arena_bytes = 16;
+      for (size_t i = 0; i < n; ++i) {
+        if (!fgets(line, sizeof line, stdin)) return 3;
+        const char* h = strtok(line, " \n");
+        g_glen[i] = (h && strcmp(h, "-") != 0) ? strlen(h) / 2 : 0;
+        g_gb[i] = malloc(g_glen[i] + 1);
+        if (g_glen[i] && unhex(h, g_gb[i], g_glen[i])) return 3;
+        arena_bytes += (g_glen[i] + 15) & ~(size_t)15;
+      }
+      nwc_digester* q = nwc_digester_create(max_group, wait_us);
+      if (!q) {
+        printf("G CREATE %s\n", nwc_last_error());
+        fflush(stdout);
+        continue;
+      }
+      unsigned char* arena = use_arena ? nwc_digester_arena(q, arena_bytes) : NULL;
+      if (use_arena && !arena) return 5;
+      size_t off = 0;
+      size_t submitted = 0;
+      for (size_t i = 0; i < n; ++i) {
+        const unsigned char* src = g_gb[i];
+        if (arena) {   /* received straight into the arena, at 16-byte-rounded offsets */
+          memcpy(arena + off, g_gb[i], g_glen[i]);
+          src = arena + off;
+          off += (g_glen[i] + 15) & ~(size_t)15;
+        }
+        rc = nwc_digester_submit(q, src, g_glen[i], i);
+        if (rc != 0) {
+          printf("g %zu SUBMIT %d\n", i, rc);
+          continue;
+        }
+        ++submitted;
+      }
+      uint64_t* tags = malloc(sizeof(uint64_t) * (n + 1));
+      unsigned char* dig = malloc(32 * (n + 1));
+      size_t back = 0;
+      int idle = 0;
+      while (back < submitted && idle < 50) {
+        size_t k = 0;
+        rc = nwc_digester_poll(q, n, 100000, tags, dig, &k);
+        idle = k ? 0 : idle + 1;
+        for (size_t j = 0; j < k; ++j) {
+          if (rc == 0) {
+            printf("g %llu ", (unsigned long long)tags[j]);
+            puthex(dig + 32 * j, 32);
+            printf("\n");
+            memcpy(g_gdig + 32 * tags[j], dig + 32 * j, 32);
+          } else {
+            printf("g %llu ERR %d\n", (unsigned long long)tags[j], rc);
+          }
+        }
+        back += k;
+        if (rc != 0 && k == 0) break;   /* sticky error, nothing left */
+      }
+      free(tags);
+      free(dig);
+      printf("G %d\n", nwc_digester_destroy(q));
+    } else if (tok[0] == 'Y') {
+      const char* t = strtok(NULL, " \n");
+      const char* r = strtok(NULL, " \n");
+      if (!t || !r) return 3;
+      const int threads = atoi(t);
+      g_rounds = atoi(r);
+      pthread_t th[65];
+      long mism = 0;
+      int k = 0;
+      pthread_create(&th[k++], NULL, digest_streamer, NULL);
+      for (int j = 0; j < threads && k < 65; ++j) pthread_create(&th[k++], NULL, verifier, NULL);
+      for (int j = 0; j < k; ++j) {
+        void* v = NULL;
+        pthread_join(th[j], &v);
+        mism += (long)v;
+      }
+      printf("Y %ld\n", mism);
     } else if (tok[0] == 'Z') {
       /* sanitizer self-check (tests only): one byte read past a heap block must be reported */
       volatile unsigned char* z = malloc(16);
@@ -285,6 +524,14 @@ int main(void) {
     free(g_b[i].sigs);
     free(g_b[i].bad);
   }
+  for (size_t i = 0; i < g_gn; ++i) free(g_gb[i]);
+  free(g_gb);
+  free(g_glen);
+  free(g_gdig);
+  free(g_vm);
+  free(g_vp);
+  free(g_vs);
+  free(g_vbits);
   nwc_shutdown();
   return 0;
 }

@@ -47,6 +47,25 @@ def test_calls_without_init_fail_loudly():
         assert b"nwc_init" in lib.nwc_last_error()
 
 
+def test_build_id_matches_sources():
+    """libnwc.so embeds the hash of the sources it was compiled from (narwhal_amd/build.py), and
+    build() recompiles whenever they differ: the in-tree library is this tree's."""
+    from narwhal_amd import _lib, build
+    lib = _lib.load(init=False)
+    assert lib.nwc_build_id().decode() == build.source_id() == build.embedded_id()
+    assert build.up_to_date()
+
+
+def test_diag_set_rejects_bad_knobs_without_a_device():
+    from narwhal_amd import _lib
+    lib = _lib.load(init=False)
+    assert lib.nwc_diag_set(b"no_such_knob", 1) == _lib.NWC_ERR_ARG
+    assert lib.nwc_diag_set(b"straus_nq", 0) == _lib.NWC_ERR_ARG
+    assert lib.nwc_diag_set(b"straus_nq", 17) == _lib.NWC_ERR_ARG
+    assert lib.nwc_diag_set(b"force_windows", 32) == _lib.NWC_ERR_ARG
+    assert lib.nwc_diag_set(b"straus_nq", 12) == 0 and lib.nwc_diag_set(b"force_windows", 0) == 0
+
+
 def test_gfx950_code_object_present():
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", LIB], capture_output=True, text=True).stdout
     blob = open(LIB, "rb").read()

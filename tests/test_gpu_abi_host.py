@@ -1,7 +1,11 @@
 """The C ABI from a plain C host (tests/cpp/abi_host.c): no Python or torch in the verifying
 process, as in the Rust `crypto` shim of INTEGRATION.md.  Golden strict verdicts, the reference
 batch cases with their bad-vote bitmaps, and SHA-512 digests, through nwc_verify_strict /
-nwc_verify_batch / nwc_sha512_trunc32_many."""
+nwc_verify_batch / nwc_sha512_trunc32_many; and, in the AddressSanitizer + UBSan build, every
+host entry with threads or queues behind it: sharded strict and certificate calls, the Straus
+batch entry, the message pipeline, the worker digester (stages, receive arena, a failing group)
+and a digester streaming while other threads verify on the same device."""
+import hashlib
 import os
 import subprocess
 
@@ -114,8 +118,29 @@ def test_c_host_under_asan(oracle, golden_verify, golden_batch):
     ocert, obad = oracle.batch_many(dig, offs, vp, vs)
     want.append("C 0 %s %s" % (np.packbits(ocert, bitorder="little").tobytes().hex(),
                                np.packbits(obad, bitorder="little").tobytes().hex()))
+    # the same certificates through dalek's batch equation (Straus sub-batches + leaves): the
+    # deterministic domain (honest keys, corrupted signatures), so exactly the oracle's answer
+    lines.append("T %d %s" % (len(sizes), " ".join(str(int(o)) for o in offs)))
+    lines += ["%s %s" % (p.tobytes().hex(), s.tobytes().hex()) for p, s in zip(vp, vs)]
+    lines += [d.tobytes().hex() for d in dig]
+    want.append("T" + want[-1][1:])
     lines.append("X 4 3")
     want.append("X 0")
+    # Core::sanitize_* from wire bytes on the reference's fixtures and the restated negatives
+    mlines, mwant = _message_requests()
+    lines += mlines
+    want += mwant
+    # the worker digester from malloc'd batches (stage path) and from its receive arena, then
+    # one digester streaming while four threads verify on the same device
+    batches = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in
+               [0, 1, 111, 112, 127, 128, 129, 255, 256] + [int(x) for x in rng.integers(0, 150_000, 40)]]
+    for max_group, wait, arena in ((7, 0, 0), (64, 200_000, 0), (4096, 100_000, 1)):
+        lines.append("G %d %d %d %d" % (max_group, wait, arena, len(batches)))
+        lines += [b.hex() or "-" for b in batches]
+        want += ["g %d %s" % (i, hashlib.sha512(b).digest()[:32].hex()) for i, b in enumerate(batches)]
+        want.append("G 0")
+    lines.append("Y 4 2")
+    want.append("Y 0")
     env = dict(os.environ, NWC_VIRTUAL_DEVICES="3", ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([ASAN_BIN], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=600, env=env)
@@ -123,8 +148,59 @@ def test_c_host_under_asan(oracle, golden_verify, golden_batch):
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
     got = [l.rstrip() for l in r.stdout.splitlines()]
     assert len(got) == len(want), (len(got), len(want), r.stderr[-1000:])
-    mism = [(i, g[:80], w[:80]) for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    mism = [(i, g[:80], w[:80]) for i, (g, w) in enumerate(zip(got, want)) if not _same(g, w)]
     assert not mism, mism[:5]
+    # a digest group that fails on the device (NWC_DIGEST_FAIL_GROUP=2, the second launch): its
+    # tags come back with the error, the groups around it as digests, destroy reports the error
+    small = [rng.integers(0, 256, 1000 + 10 * i, dtype=np.uint8).tobytes() for i in range(12)]
+    fl = ["G 4 2000000 0 12"] + [b.hex() for b in small]
+    fw = ["g %d %s" % (i, hashlib.sha512(b).digest()[:32].hex()) if not 4 <= i < 8 else "g %d ERR -1" % i
+          for i, b in enumerate(small)] + ["G -1"]
+    r = subprocess.run([ASAN_BIN], input="\n".join(fl) + "\n", capture_output=True, text=True, timeout=300,
+                       env=dict(env, NWC_DIGEST_FAIL_GROUP="2"))
+    assert r.returncode == 0 and "AddressSanitizer" not in r.stderr, (r.returncode, r.stderr[-3000:])
+    assert [l.rstrip() for l in r.stdout.splitlines()] == fw, r.stdout[-2000:]
     # the sanitizer is live in this process layout: an out-of-bounds heap read is reported
     r = subprocess.run([ASAN_BIN], input="Z\n", capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "heap-buffer-overflow" in r.stderr, (r.returncode, r.stderr[-500:])
+
+
+def _same(got: str, want) -> bool:
+    """A line equal to the expected text, or an M line matching a checker function."""
+    return want(got) if callable(want) else got == want
+
+
+def _message_requests():
+    """Q (committee config) + one M request per (gc_round, target) group of the golden message
+    fixtures (tests/golden/messages.json), with a checker per M line: codes always, the digest and
+    kind where the fixture has them."""
+    import json
+    from tests.conftest import GOLDEN
+    g = json.load(open(os.path.join(GOLDEN, "messages.json")))
+    c = g["committee"]
+    lines = ["Q %d" % len(c["keys"])]
+    lines += ["%s %d %d %s" % (k, st, len(w), " ".join(str(x) for x in w)) for k, st, w in
+              zip(c["keys"], c["stakes"], c["workers"])]
+    want = ["Q 0"]
+    groups = {}
+    for case in g["cases"]:
+        groups.setdefault((case["gc_round"], json.dumps(case["target"])), []).append(case)
+    for (gc, tj), cases in groups.items():
+        t = json.loads(tj)
+        target = "-" if t is None else t[0] + int(t[1]).to_bytes(8, "little").hex() + t[2]
+        lines.append("M %d %d %s" % (len(cases), gc, target))
+        lines += [x["msg"] or "-" for x in cases]
+
+        def check(line, cases=cases):
+            parts = line.split()
+            if parts[:2] != ["M", "0"] or len(parts) != 2 + len(cases):
+                return False
+            for case, item in zip(cases, parts[2:]):
+                code, kind, dg = item.split(",")
+                if int(code) != case["code"]:
+                    return False
+                if case["kind"] >= 0 and case["kind"] != 3 and (int(kind) != case["kind"] or dg != case["digest"]):
+                    return False
+            return True
+        want.append(check)
+    return lines, want

@@ -1,0 +1,152 @@
+"""Device memory per process and the digester's failure path (include/nwc.h nwc_memory_info,
+nwc_trim, NWC_DIGEST_MAX_BYTES / NWC_DIGEST_KEEP_BYTES, NWC_DIGEST_FAIL_GROUP), and the build id
+of the library the GPU runs.
+
+The reference's Processor hashes one batch at a time (worker/src/processor.rs:35-55) and holds
+nothing between batches; a primary and a worker may share one GPU, so the library must not keep a
+large group's buffer resident, and a group that fails on the device must hand its batches back
+(the caller holds them) instead of orphaning them."""
+import hashlib
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+BATCH = 508_052   # BASELINE config 4's batch (977 txs of 512 B, bincode)
+
+
+def _sha32(b) -> bytes:
+    return hashlib.sha512(bytes(b)).digest()[:32]
+
+
+def _digester_with_env(env, max_group, wait_us):
+    """A Digester created with `env` set: the digester reads its NWC_DIGEST_* knobs at create."""
+    from narwhal_amd.processor import Digester
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Digester(max_group, wait_us)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+
+
+def _drain(dg, n, timeout=120):
+    got, t0 = [], time.time()
+    while len(got) < n and time.time() - t0 < timeout:
+        got += dg.poll(4096, 100_000)
+    return got
+
+
+def test_build_id_is_this_trees():
+    """The library the GPU loads was compiled from the sources in this tree (a stale prebuilt
+    .so would carry another hash)."""
+    from narwhal_amd import _lib, build
+    lib = _lib.load()
+    assert lib.nwc_build_id().decode() == build.source_id()
+    print("libnwc build id", build.source_id())
+
+
+def test_large_group_is_released_and_small_one_fits():
+    """A group above NWC_DIGEST_KEEP_BYTES leaves no device buffer behind; a later small group
+    keeps only its own; digests equal hashlib throughout."""
+    from narwhal_amd import _lib
+    rng = np.random.default_rng(11)
+    batch = rng.integers(0, 256, BATCH, dtype=np.uint8)
+    want = _sha32(batch)
+    dg = _digester_with_env({"NWC_DIGEST_KEEP_BYTES": str(256 << 20)}, 100_000, 200_000)
+    try:
+        n_big = 1200   # 610 MB of batches (the same borrowed buffer, one launch)
+        for i in range(n_big):
+            dg.submit(batch, i)
+        got = _drain(dg, n_big)
+        assert len(got) == n_big and all(d == want for _, d in got)
+        assert _lib.memory_info()["digesters"] < (1 << 20), _lib.memory_info()
+        small = [rng.integers(0, 256, int(k), dtype=np.uint8) for k in rng.integers(1, 50_000, 20)]
+        for i, b in enumerate(small):
+            dg.submit(b, n_big + i)
+        got = _drain(dg, len(small))
+        assert [d for _, d in got] == [_sha32(b) for b in small]
+        held = _lib.memory_info()["digesters"]
+        assert 0 < held < (64 << 20), held
+        groups, nb, _ = dg.stats()
+        assert nb == n_big + len(small)
+    finally:
+        dg.close()
+    assert _lib.memory_info()["digesters"] == 0
+
+
+def test_group_bytes_capped_per_launch():
+    """NWC_DIGEST_MAX_BYTES cuts a group that would exceed it into several launches (in order)."""
+    rng = np.random.default_rng(12)
+    batches = [rng.integers(0, 256, BATCH, dtype=np.uint8) for _ in range(8)]
+    dg = _digester_with_env({"NWC_DIGEST_MAX_BYTES": str(2 * BATCH + 64)}, 1000, 300_000)
+    try:
+        for i in range(40):
+            dg.submit(batches[i % 8], i)
+        got = _drain(dg, 40)
+        assert [t for t, _ in got] == list(range(40))
+        assert all(d == _sha32(batches[t % 8]) for t, d in got)
+        groups, nb, _ = dg.stats()
+        assert nb == 40 and groups >= 20, groups   # at most two batches per launch
+    finally:
+        dg.close()
+
+
+def test_failed_group_returns_its_tags():
+    """NWC_DIGEST_FAIL_GROUP=2: the second launch fails.  Its batches come back as tags with the
+    error (DigestGroupError.tags), the groups before and after it as digests, in order; then
+    submit refuses new batches and poll keeps reporting the error."""
+    from narwhal_amd import _lib
+    from narwhal_amd.processor import DigestGroupError
+    rng = np.random.default_rng(13)
+    batches = [rng.integers(0, 256, 1000 + 100 * i, dtype=np.uint8) for i in range(12)]
+    dg = _digester_with_env({"NWC_DIGEST_FAIL_GROUP": "2"}, 4, 2_000_000)
+    try:
+        for i, b in enumerate(batches):
+            dg.submit(b, 100 + i)
+        ok, failed, t0 = [], [], time.time()
+        while len(ok) + len(failed) < 12 and time.time() - t0 < 60:
+            try:
+                ok += dg.poll(4096, 100_000)
+            except DigestGroupError as e:
+                assert e.tags, "an error with no tags before every batch came back"
+                failed += e.tags
+        assert failed == [104, 105, 106, 107], failed
+        assert [t for t, _ in ok] == [100, 101, 102, 103, 108, 109, 110, 111]
+        assert all(d == _sha32(batches[t - 100]) for t, d in ok)
+        with pytest.raises(_lib.DeviceError):
+            dg.submit(batches[0], 999)
+        with pytest.raises(DigestGroupError) as ei:
+            dg.poll(16, 0)
+        assert ei.value.tags == []
+        assert not dg._held   # every batch was released back to the caller
+    finally:
+        with pytest.raises(_lib.DeviceError):
+            dg.close()   # destroy reports the sticky error
+
+
+def test_trim_releases_scratch():
+    """nwc_trim frees the on-demand scratch; the next call re-allocates it and verdicts hold."""
+    import torch
+    from narwhal_amd import _lib, device
+    n = 1 << 15
+    msgs = device.derive32(b"trim-msg", 0, n)
+    pks, sigs = device.keygen_sign(device.derive32(b"trim-seed", 0, n), msgs)
+    sigs[::7, 40] ^= 1
+    first = device.unpack_bits(device.verify(msgs, pks, sigs, strict=True), n)
+    torch.cuda.synchronize()
+    before = _lib.memory_info()
+    assert before["scratch"] > 0 and before["tables"] > (2 << 30)
+    _lib.check(_lib.load().nwc_trim())
+    after = _lib.memory_info()
+    assert after["scratch"] < before["scratch"] and after["tables"] == before["tables"]
+    again = device.unpack_bits(device.verify(msgs, pks, sigs, strict=True), n)
+    torch.cuda.synchronize()
+    assert (again == first).all() and first.sum() == n - (n + 6) // 7

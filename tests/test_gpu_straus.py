@@ -74,7 +74,7 @@ def test_golden_batches_straus(golden_batch):
 def test_certificates_vs_oracle(oracle, big):
     """Honest and 1 %-bad certificates of many sizes (empty, single-vote, and 383 / 1,600 votes: the
     sub-batches cut across certificate boundaries everywhere).  Verdicts and bad sets equal the
-    oracle's, at the default sub-batch size and at 1 and 16 votes per sub-batch."""
+    oracle's, at the default sub-batch size and at 1 and 16 votes per sub-batch (nwc_diag_set)."""
     rng = np.random.default_rng(41)
     sizes = [0, 1, 2, 3, 24, 25, 48, 49, 67, 67, 67, 100, 200, big] + [int(x) for x in rng.integers(1, 90, 120)]
     m = len(sizes)
@@ -90,15 +90,13 @@ def test_certificates_vs_oracle(oracle, big):
     bad = rng.random(nv) < 0.01
     sigs[bad, 33] ^= 1
     ocert, obad = oracle.batch_many(dig, offs.astype(np.uint32), pks, sigs)
-    for nq in (None, "1", "16"):
-        if nq is None:
-            os.environ.pop("NWC_STRAUS_NQ", None)
-        else:
-            os.environ["NWC_STRAUS_NQ"] = nq
+    from narwhal_amd import _lib
+    for nq in (12, 1, 16):   # the default first
+        _lib.diag_set("straus_nq", nq)
         try:
             cert, gbad = _run(dig, offs, pks, sigs)
         finally:
-            os.environ.pop("NWC_STRAUS_NQ", None)
+            _lib.diag_set("straus_nq", 12)
         assert (cert == ocert).all(), (nq, np.nonzero(cert != ocert))
         assert (gbad == obad).all(), nq
     assert ocert.sum() > m // 3 and (~ocert).sum() > 3

@@ -7,7 +7,7 @@ searched among device-generated signatures (the host restatement of the reductio
 is placed in a wave of its own with 63 ordinary triples, a quarter of all triples are corrupted, and
 the verdicts are compared with the oracle (dalek verify_strict restated).  Natural 136+-bit lanes
 (W >= 35) are rarer than 1 in 10^6, so W = 34..37 are also forced on ordinary batches through the
-NWC_FORCE_WINDOWS test hook (extra top windows carry zero digits; the verdicts must not change).
+nwc_diag_set("force_windows") test hook (extra top windows carry zero digits; the verdicts must not change).
 """
 import ctypes
 import hashlib
@@ -101,7 +101,8 @@ def test_forced_windows(oracle, W):
     for i in np.nonzero(rng.random(n) < 0.25)[0]:
         col = rng.integers(0, 64)
         s[i, col] ^= 1 << rng.integers(0, 8 if col < 63 else 4)
-    os.environ["NWC_FORCE_WINDOWS"] = str(W)
+    from narwhal_amd import _lib
+    _lib.diag_set("force_windows", W)
     try:
         got = {}
         for strict in (True, False):
@@ -110,7 +111,7 @@ def test_forced_windows(oracle, W):
             torch.cuda.synchronize()
             got[strict] = device.unpack_bits(words, n)
     finally:
-        del os.environ["NWC_FORCE_WINDOWS"]
+        _lib.diag_set("force_windows", 0)
     assert (got[True] == oracle.strict_many(m, p, s)).all()
     assert (got[False] == oracle.leaf_many(m, p, s)).all()
     assert 0.6 * n < got[True].sum() < 0.9 * n

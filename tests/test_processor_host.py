@@ -55,3 +55,69 @@ def test_processor_order_and_messages():
         assert got == want and tx.empty()
         assert got[0][:4] == struct.pack("<I", 0 if own else 1) and got[0][-4:] == struct.pack("<I", 9)
         assert all(store[hashlib.sha512(b).digest()[:32]] == b for b in batches)
+
+
+class Store(dict):
+    def write(self, k, v):
+        self[k] = v
+
+
+def test_submit_error_is_raised_by_join():
+    """A digester whose submit raises (a bad batch type, a failed C submit): the feeder records
+    the error, the collector stops instead of waiting for batches that were never queued, and
+    join() raises it (_submitted was counted before submit, so join hung)."""
+    class Failing(GroupedDigester):
+        def submit(self, batch, tag):
+            if tag == 3:
+                raise TypeError("unsupported buffer type")
+            super().submit(batch, tag)
+
+    dg = Failing()
+    p = Processor(1, Store(), queue.Queue(), queue.Queue(), True, digester=dg)
+    for i in range(6):
+        p.rx.put(bytes([i]) * 10)
+    p.rx.put(None)
+    try:
+        p.join(10)
+        raise AssertionError("join() did not raise")
+    except TypeError as e:
+        assert "unsupported" in str(e)
+    assert p._submitted == 3 and 3 not in p._pending
+
+
+def test_join_timeout_keeps_the_digester():
+    """join(timeout) while the collector is still inside poll must not free the digester under
+    it (use-after-free in nwc_digester_destroy): it raises TimeoutError instead."""
+    class Slow(GroupedDigester):
+        def poll(self, max_n=4096, wait_us=0):
+            import time
+            time.sleep(0.05)
+            return []   # never releases anything
+
+        def close(self):
+            raise AssertionError("closed while a poller is alive")
+
+    dg = Slow()
+    p = Processor(1, Store(), queue.Queue(), queue.Queue(), True, digester=dg)
+    p.rx.put(b"x" * 10)
+    p.rx.put(None)
+    try:
+        p.join(0.3)
+        raise AssertionError("join() returned")
+    except TimeoutError:
+        pass
+    p._error = RuntimeError("test over")   # let the collector leave
+
+
+def test_buf_rejects_non_contiguous_arrays():
+    """A strided view would be read as nbytes contiguous bytes from its first element -- the
+    wrong bytes, silently: the binding refuses it."""
+    import numpy as np
+    from narwhal_amd import _lib
+    a = np.arange(64, dtype=np.uint8)
+    assert _lib.buf(a[::2].copy()) is not None
+    try:
+        _lib.buf(a[::2])
+        raise AssertionError("strided view accepted")
+    except TypeError:
+        pass
