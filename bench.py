@@ -346,7 +346,10 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
     """BASELINE config 3: 100-node committee, m certificates x 67 votes (quorum 2N/3+1,
     config/src/lib.rs:181-186), each vote invalid with p = 0.01 (signed over another digest).
     Leaf equations for every vote + per-certificate AND; bad-vote sets checked against the
-    construction.  Timed with and without the committee key cache."""
+    construction.  Timed without any key cache (the per-vote ladder; dalek's batch equation over
+    sub-batches), with the launch keys the library detects itself (no nwc_set_committee: first
+    launch incl. the census and the 100 keys' comb builds, then steady state), and with the
+    committee key cache."""
     from narwhal_amd import _lib, device
     import torch
     N, Q = 100, 67
@@ -371,8 +374,11 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
     out = {}
     legs = (("no_cache", False, "leaf", pks, sigs, bad), ("no_cache_straus", False, "straus", pks, sigs, bad),
             ("clean_no_cache", False, "leaf", clean_pks, clean_sigs, no_bad),
-            ("clean_no_cache_straus", False, "straus", clean_pks, clean_sigs, no_bad), ("cache", True, "leaf", pks, sigs, bad))
+            ("clean_no_cache_straus", False, "straus", clean_pks, clean_sigs, no_bad),
+            ("launch_keys", False, "launch", pks, sigs, bad), ("cache", True, "leaf", pks, sigs, bad))
     for tag, use_cache, eq, P, S, want_bad in legs:
+        _lib.check(lib.nwc_set_committee(None, 0))   # no committee cache, launch keys emptied
+        _lib.diag_set("launch_keys", 1 if eq == "launch" else 0)
         if use_cache:
             cpk = committee_pks.cpu().numpy()
             _lib.check(lib.nwc_set_committee(_lib.buf(cpk), N))
@@ -383,8 +389,10 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
         else:
             run = lambda: device.cert_reduce(device.verify(cdig, P, S, strict=False, msg_index=msg_index,  # noqa
                                                            out=words), offs, nv)
+        t0 = time.perf_counter()
         run()
         torch.cuda.synchronize()
+        first_ms = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
         for _ in range(steps):
             cw, bw = run()
@@ -395,9 +403,17 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
         cert_ok = torch.from_numpy(device.unpack_bits(cw, m)).cuda()
         ok = ok and bool((cert_ok == ~want_bad.view(m, Q).any(dim=1)).all())
         out[tag] = {"votes_per_s": nv / dt, "certs_per_s": m / dt, "ms_per_step": dt * 1e3, "parity_ok": ok,
-                    "equation": "dalek batch equation over sub-batches of ~12 votes (Straus per lane), leaves for failing sub-batches"
-                    if eq == "straus" else "per-vote leaves", "bad_rate": 0.01 if want_bad is bad else 0.0}
+                    "first_call_ms": first_ms,
+                    "equation": {"straus": "dalek batch equation over sub-batches of ~12 votes (Straus per lane), leaves for failing sub-batches",
+                                 "launch": "per-vote leaves; the launch's repeated keys detected by the library (no nwc_set_committee), "
+                                           "their combs built on the first call, comb kernel from then on"}.get(eq, "per-vote leaves"),
+                    "bad_rate": 0.01 if want_bad is bad else 0.0}
+        if eq == "launch":
+            h = ctypes.c_uint32()
+            _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
+            out[tag]["launch_keys_held"] = h.value
     _lib.check(lib.nwc_set_committee(None, 0))
+    _lib.diag_set("launch_keys", 1)
     if cpu_budget > 0:
         out["cpu_baseline"] = cpu_baseline_cfg3(cdig, pks, sigs, m, Q, bad, cpu_budget)
     out["workload"] = "cfg3: %d certificates x %d votes, 1%% invalid, leaf equations + certificate AND + bad-vote set" % (m, Q)

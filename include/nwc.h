@@ -68,7 +68,8 @@ int nwc_trim(void);
 /* Test / A-B knobs, settable at run time instead of through the environment (which is read
  * once): "straus_nq" = votes per sub-batch of nwc_dev_verify_batch_straus (1..16, default 12,
  * env NWC_STRAUS_NQ); "force_windows" = half-ladder windows forced on every wave (33..37, 0 = off,
- * env NWC_FORCE_WINDOWS; verdicts must not change).  NWC_ERR_ARG for an unknown name or value.
+ * env NWC_FORCE_WINDOWS; verdicts must not change); "launch_keys" = 0 / 1 (default 1, env
+ * NWC_LAUNCH_KEYS; nwc_launch_keys_info).  NWC_ERR_ARG for an unknown name or value.
  * Not part of the crate's API. */
 int nwc_diag_set(const char* name, int64_t value);
 
@@ -121,6 +122,15 @@ int nwc_cache_stats(uint32_t* committee_keys, uint32_t* auto_keys);
  * Diagnostics only, not part of the crate's API. */
 int nwc_auto_cache_info(uint32_t* capacity, uint64_t* builds, uint64_t* hits);
 
+/* Launch keys of the calling thread's device: a batch-leaf launch of >= 65,536 equations without a
+ * committee cache samples its keys, and keys it repeats (>= ~1/4096 of the sample) join a
+ * device-resident set with their flags and radix-2^14 combs (built once), so that votes of a
+ * committee the caller never registered take the comb kernel -- cross-certificate key
+ * aggregation, no nwc_set_committee needed.  Append-only up to `capacity` keys; emptied by
+ * nwc_set_committee; NWC_LAUNCH_KEYS=0 (or nwc_diag_set("launch_keys", 0)) turns it off.
+ * Verdicts never depend on it.  Waits for the device.  Diagnostics only. */
+int nwc_launch_keys_info(uint32_t* held, uint32_t* capacity);
+
 /* ---- worker batch digests behind a Processor-shaped queue (worker/src/processor.rs:35-55) ----
  * Replaces the Processor's per-batch `Sha512::digest(&batch)[..32]` (:38) for workers that can
  * hand batches over in groups.  A digester owns a drain thread on the calling thread's device
@@ -138,8 +148,8 @@ int nwc_auto_cache_info(uint32_t* capacity, uint64_t* builds, uint64_t* hits);
  * (nwc_last_error).  poll waits up to wait_us for a result and returns one run of results with
  * the same status: digests (returns 0), or the tags of a group that failed on the device (returns
  * the error code < 0; digests32 zeroed) -- every submitted tag comes back exactly once, in order.
- * After a failure submit refuses new batches, and poll returns the error (n_done = 0) once
- * nothing is left to hand back.  destroy digests what is queued, wakes threads blocked in poll and
+ * After a failure submit refuses new batches, and poll returns the error (n_done = 0) once every
+ * batch submitted before it has come back.  destroy digests what is queued, wakes threads blocked in poll and
  * waits for them to leave, then frees the digester (no call on it may start after destroy). */
 typedef struct nwc_digester nwc_digester;
 nwc_digester* nwc_digester_create(uint32_t max_group, uint32_t max_wait_us);

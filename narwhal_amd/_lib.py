@@ -42,6 +42,7 @@ _SIGS = {
     "nwc_set_committee": (ctypes.c_int, [_c_u8p, ctypes.c_size_t]),
     "nwc_cache_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_auto_cache_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "nwc_launch_keys_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_digest32": (ctypes.c_int, [_c_u8p, ctypes.c_size_t, _c_u8p]),
     "nwc_sha512_trunc32_many": (ctypes.c_int, [_c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p]),
     "nwc_dev_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,

@@ -103,6 +103,7 @@ struct Digester {
   std::string err_msg;
   bool stop = false;
   uint64_t groups = 0, batches = 0, bytes = 0, submitted = 0, launched = 0;
+  uint64_t returned = 0;           // results pushed to `out` (ok or failed); submitted - returned are in flight
   std::thread th;
   CopyPool pool;
   std::chrono::steady_clock::time_point t_group;   // first batch of the current group taken (timing)
@@ -312,6 +313,7 @@ struct Digester {
       // every tag comes back, in order: a failed group's with its error code and no digest
       for (size_t i = 0; i < g.size(); ++i) {
         out.push_back(Item{nullptr, g[i].len, g[i].tag, rc});
+        ++returned;
         std::array<uint8_t, 32> a{};
         if (!rc) std::memcpy(a.data(), dig.data() + 32 * i, 32);
         out_dig.push_back(a);
@@ -409,8 +411,10 @@ int nwc_digester_poll(nwc_digester* h, size_t max, uint32_t wait_us, uint64_t* t
   if (!q || !n_done || (max && (!tags || !digests32))) return set_err(NWC_ERR_ARG, "null argument");
   std::unique_lock<std::mutex> lk(q->mu);
   ++q->pollers;
-  if (wait_us && q->out.empty() && !q->err && !q->stop)
-    q->cv_out.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return !q->out.empty() || q->err || q->stop; });
+  // the sticky error stands alone only once every submitted batch has come back
+  auto drained_err = [&] { return q->err && q->returned == q->submitted; };
+  if (wait_us && q->out.empty() && !drained_err() && !q->stop)
+    q->cv_out.wait_for(lk, std::chrono::microseconds(wait_us), [&] { return !q->out.empty() || drained_err() || q->stop; });
   // a run of results with one status: digests (rc 0) or a failed group's tags (rc < 0)
   const int status = q->out.empty() ? 0 : q->out.front().status;
   size_t n = 0;
@@ -424,7 +428,7 @@ int nwc_digester_poll(nwc_digester* h, size_t max, uint32_t wait_us, uint64_t* t
   *n_done = n;
   int rc = 0;
   if (status) rc = set_err(status, "digest group failed: %s", q->err_msg.c_str());
-  else if (n == 0 && q->err) rc = set_err(q->err, "%s", q->err_msg.c_str());   // sticky, nothing left to hand back
+  else if (n == 0 && drained_err()) rc = set_err(q->err, "%s", q->err_msg.c_str());   // sticky, nothing left to hand back
   if (--q->pollers == 0) q->cv_idle.notify_all();
   return rc;
 }

@@ -1409,9 +1409,18 @@ __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs c
       const u32 fl = cm.flags[kk];
       const bool small = a.strict && ycanon_is_small_order(r.yr);
       const bool ok = active && key >= 0 && sc_lt_l(sw) && key_flags_ok(fl, a.strict != 0) && !small;
-      u32 kw[8];
-      challenge(rw, aw, mw, kw);
-      const ge_p2 q = comb_sum(sw, kw, ca.comb16, cm.comb + (size_t)kk * COMB_PER_KEY);
+      ge_p2 q;
+      if (__any(key >= 0)) {
+        u32 kw[8];
+        challenge(rw, aw, mw, kw);
+        q = comb_sum(sw, kw, ca.comb16, cm.comb + (size_t)kk * COMB_PER_KEY);
+      } else {
+        // no equation of this wave has a cached key (launch keys: another committee's votes, or a
+        // launch without repeated keys): skip the sum, the list-mode ladder decides them all
+        q.X = fe_zero();
+        q.Y = fe_one();
+        q.Z = fe_one();
+      }
       // Z != 0 for every sum of curve points (complete formulas); a key that does not decode has
       // an off-curve comb, whose Z must not zero the lane's batched inversion
       const bool zbad = fe_is_zero(q.Z);

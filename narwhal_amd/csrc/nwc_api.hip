@@ -26,6 +26,7 @@
 
 #include "nwc.h"
 #include "kernels.hip"
+#include "launch_keys.h"
 #include "messages.h"
 
 namespace {
@@ -178,6 +179,9 @@ struct DevCtx {
   std::vector<nwc::u32> ak_pend_keys;
   std::vector<int32_t> ak_pend_slots;
   bool ak_pending = false;
+  // launch keys (launch_keys.h): allocated by the first large batch-leaf launch without a committee
+  nwc::LaunchKeys lk{};
+  bool lk_alloc = false;
   std::mutex mu;
 
   int ensure_pinned(size_t bytes) {
@@ -262,7 +266,9 @@ bool comb16_enabled();
 struct Knobs {
   std::atomic<uint32_t> straus_nq{12};
   std::atomic<uint32_t> force_windows{0};
+  std::atomic<uint32_t> launch_keys{1};   // NWC_LAUNCH_KEYS: 0 = large batch-leaf launches never build launch keys
   Knobs() {
+    if (const char* e = std::getenv("NWC_LAUNCH_KEYS")) launch_keys = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("NWC_STRAUS_NQ")) straus_nq = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("NWC_FORCE_WINDOWS")) force_windows = (uint32_t)std::strtoul(e, nullptr, 10);
   }
@@ -625,6 +631,23 @@ uint64_t cold_max() {
   return m;
 }
 
+// Device buffers of the launch keys (launch_keys.h), allocated once per device; the set starts
+// empty.  Caller holds d.mu.
+int lk_ensure(DevCtx& d, hipStream_t s) {
+  if (d.lk_alloc) return 0;
+  nwc::LaunchKeys& k = d.lk;
+  HIP_TRY(hipMalloc(&k.keys, 32 * (size_t)nwc::LK_MAX_KEYS));
+  HIP_TRY(hipMalloc(&k.flags, 4 * (size_t)nwc::LK_MAX_KEYS));
+  HIP_TRY(hipMalloc(&k.slots, 4 * (size_t)nwc::LK_SLOTS));
+  HIP_TRY(hipMalloc(&k.comb, (size_t)nwc::LK_MAX_KEYS * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad)));
+  HIP_TRY(hipMalloc(&k.bases, (size_t)nwc::LK_MAX_KEYS * nwc::KeyComb::windows * sizeof(nwc::ge_p3)));
+  HIP_TRY(hipMalloc(&k.state, 16));
+  HIP_TRY(hipMemsetAsync(k.slots, 0xFF, 4 * (size_t)nwc::LK_SLOTS, s));
+  HIP_TRY(hipMemsetAsync(k.state, 0, 16, s));
+  d.lk_alloc = true;
+  return 0;
+}
+
 // launch_verify flags: the caller checked on the host that every key is in the committee cache,
 // and/or out_words is already zero (both let the latency path run as a single kernel)
 constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4;   // LV_AUTO: the keys are in the auto cache
@@ -663,7 +686,11 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     return 0;
   }
   // (the throughput comb kernel needs the basepoint comb16; the latency kernel does not)
-  const bool comb = path == VPath::Default && d.cm_n && d.cm_comb && (n <= NWC_WIDE_MAX || d.comb16);
+  // A large batch-leaf launch without a committee cache brings its own committee: the keys it
+  // repeats join the launch-key set and its votes take the comb kernel (launch_keys.h).
+  const bool lk = path == VPath::Default && !strict && !d.cm_n && d.comb16 && n >= nwc::LK_MIN_EQUATIONS &&
+                  knobs().launch_keys.load() && !(flags & LV_AUTO);
+  const bool comb = lk || (path == VPath::Default && d.cm_n && d.cm_comb && (n <= NWC_WIDE_MAX || d.comb16));
   if (comb && n <= NWC_WIDE_MAX && (flags & LV_ALL_CACHED)) {
     // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none).
     // The host checked every key against its view of the cache (set under g_cm_mu, like the
@@ -694,8 +721,20 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     need = std::max(need, (size_t)resident * 256 * nwc::COMB_BYTES_PER_LANE);
   }
   if (int rc = ensure_scratch(d, need, n)) return rc;
+  if (lk)
+    if (int rc = lk_ensure(d, s)) return rc;
   HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
-  const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
+  if (lk) {
+    // the set's update is ordered after every launch that read it (scratch_free) and before this
+    // launch's comb kernel; the builds exit at once when no key joined
+    hipLaunchKernelGGL(nwc::k_lk_select, dim3(1), dim3(1024), 0, s, pks, n, d.lk);
+    hipLaunchKernelGGL(nwc::k_lk_keys, dim3((nwc::LK_MAX_KEYS + 63) / 64), dim3(64), 0, s, d.lk);
+    hipLaunchKernelGGL(nwc::k_lk_comb, dim3((unsigned)(d.cus * 16)), dim3(256), 0, s, d.lk);
+    HIP_TRY(hipGetLastError());
+  }
+  const nwc::Committee cm = lk ? nwc::Committee{d.lk.keys, d.lk.flags, nullptr, d.lk.comb, d.lk.slots, nwc::LK_SLOTS - 1,
+                                                nwc::LK_MAX_KEYS}
+                               : nwc::Committee{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
   nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
   a.force_windows = knobs().force_windows.load();
@@ -1159,6 +1198,9 @@ int nwc_diag_set(const char* name, int64_t value) {
   if (std::strcmp(name, "straus_nq") == 0) {
     if (value < 1 || value > nwc::STRAUS_MAX_PER_LANE) return set_err(NWC_ERR_ARG, "straus_nq must be in [1, %d]", nwc::STRAUS_MAX_PER_LANE);
     knobs().straus_nq = (uint32_t)value;
+  } else if (std::strcmp(name, "launch_keys") == 0) {
+    if (value > 1) return set_err(NWC_ERR_ARG, "launch_keys must be 0 or 1");
+    knobs().launch_keys = (uint32_t)value;
   } else if (std::strcmp(name, "force_windows") == 0) {
     if (value != 0 && (value < nwc::HALF_WINDOWS_MIN || value > nwc::HALF_WINDOWS_MAX))
       return set_err(NWC_ERR_ARG, "force_windows must be 0 or in [%d, %d]", nwc::HALF_WINDOWS_MIN, nwc::HALF_WINDOWS_MAX);
@@ -1227,6 +1269,14 @@ void nwc_shutdown(void) {
     if (d->comb16_bases) (void)hipFree(d->comb16_bases);
     if (d->kb_bases) (void)hipFree(d->kb_bases);
     if (d->straus_scratch) (void)hipFree(d->straus_scratch);
+    if (d->lk_alloc) {
+      (void)hipFree(d->lk.keys);
+      (void)hipFree(d->lk.flags);
+      (void)hipFree(d->lk.slots);
+      (void)hipFree(d->lk.comb);
+      (void)hipFree(d->lk.bases);
+      (void)hipFree(d->lk.state);
+    }
     if (d->pinned) (void)hipHostFree(d->pinned);
     if (d->cc_stakes) (void)hipFree(d->cc_stakes);
     if (d->cc_worker_off) (void)hipFree(d->cc_worker_off);
@@ -1390,6 +1440,10 @@ static int set_committee_locked(const uint8_t* pks, size_t n) {
     HIP_TRY(hipEventSynchronize(d.scratch_free));   // no verify launch still reads the old cache
     HIP_TRY(hipStreamSynchronize(d.stream));
     auto_reset(d);   // keys remembered under the old committee are stale
+    if (d.lk_alloc) {   // so are the launch keys
+      HIP_TRY(hipMemsetAsync(d.lk.slots, 0xFF, 4 * (size_t)nwc::LK_SLOTS, d.stream));
+      HIP_TRY(hipMemsetAsync(d.lk.state, 0, 16, d.stream));
+    }
     if (d.cm_keys) HIP_TRY(hipFree(d.cm_keys));
     if (d.cm_flags) HIP_TRY(hipFree(d.cm_flags));
     if (d.cm_tables) HIP_TRY(hipFree(d.cm_tables));
@@ -1441,6 +1495,21 @@ int nwc_cache_stats(uint32_t* committee_keys, uint32_t* auto_keys) {
   std::lock_guard<std::mutex> lk(d.mu);
   if (committee_keys) *committee_keys = d.cm_n;
   if (auto_keys) *auto_keys = d.ak_n;
+  return 0;
+}
+
+int nwc_launch_keys_info(uint32_t* held, uint32_t* capacity) {
+  if (int rc = require_init()) return rc;
+  DevCtx& d = *ctx(t_dev < (int)g_devs.size() ? t_dev : 0);
+  std::lock_guard<std::mutex> g(d.mu);
+  uint32_t st[4] = {0, 0, 0, 0};
+  if (d.lk_alloc) {
+    HIP_TRY(hipSetDevice(d.hip_id));
+    HIP_TRY(hipDeviceSynchronize());   // the set is updated on callers' streams
+    HIP_TRY(hipMemcpy(st, d.lk.state, 16, hipMemcpyDeviceToHost));
+  }
+  if (held) *held = st[0];
+  if (capacity) *capacity = nwc::LK_MAX_KEYS;
   return 0;
 }
 
@@ -1817,7 +1886,11 @@ int nwc_memory_info(nwc_memory* out) {
                   36 * (size_t)NWC_MEMO_SLOTS;
     out->committee = d.cm_bytes;
     out->auto_cache = (size_t)d.ak_cap * (36 + 129 * sizeof(nwc::ge_niels) + nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad)) +
-                      4 * (size_t)d.ak_slot_cap + d.kb_cap * sizeof(nwc::ge_p3);
+                      4 * (size_t)d.ak_slot_cap + d.kb_cap * sizeof(nwc::ge_p3) +
+                      (d.lk_alloc ? (size_t)nwc::LK_MAX_KEYS * (36 + nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad) +
+                                                               nwc::KeyComb::windows * sizeof(nwc::ge_p3)) +
+                                        4 * (size_t)nwc::LK_SLOTS + 16
+                                  : 0);
     out->scratch = d.scratch_cap + d.straus_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap +
                    8 * (size_t)d.ts_slot_count;
   }

@@ -48,7 +48,7 @@ struct StrausArgs {
   uint64_t runs;              // sub-batch r = votes [r nv / runs, (r + 1) nv / runs), <= STRAUS_MAX_PER_LANE each
   uint32_t seed[8];
   const ge_niels_pad* comb16; // radix-2^22 basepoint comb
-  uint8_t* scratch;           // lane_stride bytes per lane slot (vote-major: [vote of run][lane slot])
+  uint8_t* scratch;           // lane_stride bytes per lane slot (lane-major: [lane slot][vote of run])
   uint64_t lane_stride;       // max votes per run * STRAUS_VOTE_BYTES
   uint64_t* leaf_words;       // bit v = vote v's sub-batch passed (zeroed by the caller)
   uint32_t* list;             // votes of the sub-batches that failed (for the exact leaves)

@@ -44,6 +44,7 @@ extern "C" {
     pub fn nwc_set_committee(pks: *const u8, n: usize) -> c_int;
     pub fn nwc_cache_stats(committee_keys: *mut u32, auto_keys: *mut u32) -> c_int;
     pub fn nwc_auto_cache_info(capacity: *mut u32, builds: *mut u64, hits: *mut u64) -> c_int;
+    pub fn nwc_launch_keys_info(held: *mut u32, capacity: *mut u32) -> c_int;
 
     pub fn nwc_set_committee_config(pks: *const u8, stakes: *const u64, n: usize, worker_offsets: *const u32,
                                     worker_ids: *const u32) -> c_int;

@@ -148,7 +148,7 @@ def test_c_host_under_asan(oracle, golden_verify, golden_batch):
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
     got = [l.rstrip() for l in r.stdout.splitlines()]
     assert len(got) == len(want), (len(got), len(want), r.stderr[-1000:])
-    mism = [(i, g[:80], w[:80]) for i, (g, w) in enumerate(zip(got, want)) if not _same(g, w)]
+    mism = [(i, g[:80], str(w)[:80]) for i, (g, w) in enumerate(zip(got, want)) if not _same(g, w)]
     assert not mism, mism[:5]
     # a digest group that fails on the device (NWC_DIGEST_FAIL_GROUP=2, the second launch): its
     # tags come back with the error, the groups around it as digests, destroy reports the error
