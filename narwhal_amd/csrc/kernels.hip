@@ -311,22 +311,73 @@ __global__ void k_comb_key_bases(const u32* __restrict__ keys, u32 n, ge_p3* __r
     for (int k = 0; k < S::bits; ++k) P = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
   }
 }
+// Entries of a comb window built in runs of COMB_RUN consecutive multiples per lane, with one
+// inversion per run (Montgomery's trick): entry j0 = j0 * base by double-and-add, then each next
+// entry is the previous + base; the projective (X, Y, Z) of every entry is parked in its own output
+// slot (120 of its 128 bytes) while the running product of the Z goes forward, one inversion, and
+// the backward pass turns each slot into its affine Niels form.  Per entry ~1/8 of a scalar
+// multiplication and of an inversion plus one addition and ~5 products, instead of a 14-bit
+// double-and-add and an inversion each (round 3's one-lane-per-entry builder): nwc_set_committee,
+// the auto key cache and the launch keys build their 20-MB combs this way.
+constexpr int COMB_RUN = 8;
+struct CombRunPark { fe X, Y, Z; u32 pad[2]; };
+static_assert(sizeof(CombRunPark) == sizeof(ge_niels_pad), "parked entry fits its slot");
 template <class S>
-__global__ void k_build_comb_from_bases(const ge_p3* __restrict__ bases, u32 n, ge_niels_pad* __restrict__ out) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (size_t)n * S::per) return;
-  const u32 key = (u32)(t / S::per), r = (u32)(t % S::per);
-  const int w = (int)(r / S::entries), j = (int)(r % S::entries);
-  const ge_cached pc = ge_p3_to_cached(bases[(size_t)key * S::windows + w]);
+__device__ __forceinline__ void comb_build_run(const ge_p3* __restrict__ bases, ge_niels_pad* __restrict__ out, size_t run) {
+  constexpr u32 RUNS_PER_WINDOW = (S::entries + COMB_RUN - 1) / COMB_RUN;
+  const size_t kw = run / RUNS_PER_WINDOW;   // key * windows + w
+  const u32 j0 = (u32)(run % RUNS_PER_WINDOW) * COMB_RUN;
+  const ge_p3 base = bases[kw];
+  const ge_cached pc = ge_p3_to_cached(base);
   ge_p3 acc = ge_p3_identity();
 #pragma unroll 1
   for (int bit = S::bits - 1; bit >= 0; --bit) {
     acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
-    if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, pc));
+    if ((j0 >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, pc));
   }
-  out[t].n = ge_p3_to_niels(acc);
-  out[t].pad[0] = 0;
-  out[t].pad[1] = 0;
+  ge_niels_pad* const dst = out + kw * S::entries + j0;
+  CombRunPark* const park = reinterpret_cast<CombRunPark*>(dst);
+  const int cnt = (int)min<u32>(COMB_RUN, S::entries - j0);
+  fe prod[COMB_RUN];
+  _Pragma("unroll") for (int k = 0; k < COMB_RUN; ++k) {
+    if (k < cnt) {
+      park[k].X = acc.X;
+      park[k].Y = acc.Y;
+      park[k].Z = acc.Z;
+      prod[k] = k ? fe_mul(prod[k - 1], acc.Z) : acc.Z;
+      if (k + 1 < cnt) acc = ge_p1p1_to_p3(ge_add_cached(acc, pc));
+    }
+  }
+  fe inv = fe_invert(prod[cnt - 1]);
+  _Pragma("unroll") for (int k = COMB_RUN - 1; k >= 0; --k) {
+    if (k < cnt) {
+      const fe X = park[k].X, Y = park[k].Y, Z = park[k].Z;
+      const fe zi = k ? fe_mul(inv, prod[k - 1]) : inv;
+      if (k) inv = fe_mul(inv, Z);
+      const fe x = fe_mul(X, zi), y = fe_mul(Y, zi);
+      ge_niels_pad e;
+      e.n.ypx = fe_add(y, x);
+      e.n.ymx = fe_sub(y, x);
+      e.n.xy2d = fe_mul(fe_mul(x, y), FE_D2);
+      e.pad[0] = 0;
+      e.pad[1] = 0;
+      dst[k] = e;
+    }
+  }
+}
+// Combs of keys [k0, k1) from their window bases (bases and out indexed from key 0); k0/k1 come
+// from the host, or from range[1] / range[0] on the device when range is not null (launch keys).
+template <class S>
+__global__ void k_build_comb_from_bases(const ge_p3* __restrict__ bases, u32 k0, u32 k1, const u32* range,
+                                        ge_niels_pad* __restrict__ out) {
+  constexpr u32 RUNS_PER_WINDOW = (S::entries + COMB_RUN - 1) / COMB_RUN;
+  if (range) {
+    k0 = range[1];
+    k1 = range[0];
+  }
+  const size_t lo = (size_t)k0 * S::windows * RUNS_PER_WINDOW, hi = (size_t)k1 * S::windows * RUNS_PER_WINDOW;
+  for (size_t r = lo + (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < hi; r += (size_t)gridDim.x * blockDim.x)
+    comb_build_run<S>(bases, out, r);
 }
 
 // Basepoint comb for the throughput committee kernel: comb16[w * E + j] = j * 2^(BITS w) * B,

@@ -15,7 +15,7 @@
 // set changes which kernel decides a vote, never the verdict (tests/test_gpu_launch_keys.py).
 //
 // The whole pipeline stays on the launch's stream (no host synchronisation): k_lk_select (one
-// block) updates the set, k_lk_keys / k_lk_comb build what joined (and exit at once otherwise), and
+// block) updates the set, k_lk_keys / k_build_comb_from_bases build what joined (and exit at once otherwise), and
 // k_verify_comb skips the comb sum of any wave none of whose equations has a held key.
 #pragma once
 
@@ -131,25 +131,6 @@ __global__ void k_lk_keys(LaunchKeys lk) {
     lk.bases[(size_t)q * KeyComb::windows + w] = P;
 #pragma unroll 1
     for (int k = 0; k < KeyComb::bits; ++k) P = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(P)));
-  }
-}
-
-// The combs of the keys that joined (entries as k_build_comb_from_bases), grid-stride over them.
-__global__ void k_lk_comb(LaunchKeys lk) {
-  const size_t lo = (size_t)lk.state[1] * KeyComb::per, hi = (size_t)lk.state[0] * KeyComb::per;
-  for (size_t t = lo + (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < hi; t += (size_t)gridDim.x * blockDim.x) {
-    const u32 key = (u32)(t / KeyComb::per), r = (u32)(t % KeyComb::per);
-    const int w = (int)(r / KeyComb::entries), j = (int)(r % KeyComb::entries);
-    const ge_cached pc = ge_p3_to_cached(lk.bases[(size_t)key * KeyComb::windows + w]);
-    ge_p3 acc = ge_p3_identity();
-#pragma unroll 1
-    for (int bit = KeyComb::bits - 1; bit >= 0; --bit) {
-      acc = ge_p1p1_to_p3(ge_p2_dbl(ge_p3_to_p2(acc)));
-      if ((j >> bit) & 1) acc = ge_p1p1_to_p3(ge_add_cached(acc, pc));
-    }
-    lk.comb[t].n = ge_p3_to_niels(acc);
-    lk.comb[t].pad[0] = 0;
-    lk.comb[t].pad[1] = 0;
   }
 }
 

@@ -367,9 +367,8 @@ int build_key_combs(DevCtx& d, const nwc::u32* keys, uint32_t m, nwc::ge_niels_p
   }
   hipLaunchKernelGGL(nwc::k_comb_key_bases<nwc::KeyComb>, dim3((m + 63) / 64), dim3(64), 0, d.stream, keys, m, d.kb_bases);
   HIP_TRY(hipGetLastError());
-  const size_t entries = (size_t)m * nwc::COMB_PER_KEY;
-  hipLaunchKernelGGL(nwc::k_build_comb_from_bases<nwc::KeyComb>, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0,
-                     d.stream, (const nwc::ge_p3*)d.kb_bases, m, out);
+  hipLaunchKernelGGL(nwc::k_build_comb_from_bases<nwc::KeyComb>, dim3((unsigned)(d.cus * 8)), dim3(256), 0, d.stream,
+                     (const nwc::ge_p3*)d.kb_bases, 0u, m, (const uint32_t*)nullptr, out);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -729,7 +728,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     // launch's comb kernel; the builds exit at once when no key joined
     hipLaunchKernelGGL(nwc::k_lk_select, dim3(1), dim3(1024), 0, s, pks, n, d.lk);
     hipLaunchKernelGGL(nwc::k_lk_keys, dim3((nwc::LK_MAX_KEYS + 63) / 64), dim3(64), 0, s, d.lk);
-    hipLaunchKernelGGL(nwc::k_lk_comb, dim3((unsigned)(d.cus * 16)), dim3(256), 0, s, d.lk);
+    hipLaunchKernelGGL(nwc::k_build_comb_from_bases<nwc::KeyComb>, dim3((unsigned)(d.cus * 8)), dim3(256), 0, s,
+                       (const nwc::ge_p3*)d.lk.bases, 0u, 0u, (const uint32_t*)d.lk.state, d.lk.comb);
     HIP_TRY(hipGetLastError());
   }
   const nwc::Committee cm = lk ? nwc::Committee{d.lk.keys, d.lk.flags, nullptr, d.lk.comb, d.lk.slots, nwc::LK_SLOTS - 1,

@@ -364,6 +364,7 @@ int main(void) {
       const char* tg = strtok(NULL, " \n");
       if (!cnt || !gc || !tg) return 3;
       const size_t m = (size_t)strtoul(cnt, NULL, 10);
+      const uint64_t gc_round = strtoull(gc, NULL, 10);   /* before the message lines overwrite `line` */
       unsigned char target[72];
       const int has_target = strcmp(tg, "-") != 0;
       if (has_target && unhex(tg, target, 72)) return 3;
@@ -389,7 +390,7 @@ int main(void) {
       int32_t* codes = malloc(4 * (m + 1));
       unsigned char* digs = malloc(32 * (m + 1));
       unsigned char* kinds = malloc(m + 1);
-      rc = nwc_sanitize_messages(data, offs, m, strtoull(gc, NULL, 10), has_target ? target : NULL, codes, digs, kinds);
+      rc = nwc_sanitize_messages(data, offs, m, gc_round, has_target ? target : NULL, codes, digs, kinds);
       printf("M %d", rc);
       for (size_t i = 0; rc == 0 && i < m; ++i) {
         printf(" %d,%d,", codes[i], kinds[i]);
