@@ -414,12 +414,45 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
             out[tag]["launch_keys_held"] = h.value
     _lib.check(lib.nwc_set_committee(None, 0))
     _lib.diag_set("launch_keys", 1)
+    out["host_abi_launch_keys"] = bench_cfg3_host_abi(lib, cdig, offs, pks, sigs, bad, m, Q)
     if cpu_budget > 0:
         out["cpu_baseline"] = cpu_baseline_cfg3(cdig, pks, sigs, m, Q, bad, cpu_budget)
     out["workload"] = "cfg3: %d certificates x %d votes, 1%% invalid, leaf equations + certificate AND + bad-vote set" % (m, Q)
     out["bad_votes"] = int(bad.sum().item())
     out["failing_certs"] = int(bad.view(m, Q).any(dim=1).sum().item())
     return out
+
+
+def bench_cfg3_host_abi(lib, cdig, offs, pks, sigs, bad, m: int, Q: int, reps: int = 3):
+    """Config 3 through the crate's drop-in entry: nwc_verify_batch_many from pageable host buffers
+    (certificate digests, vote offsets, 6.7M keys and signatures in; certificate and bad-vote
+    bitmaps out), no nwc_set_committee -- the launch keys pick the committee up on the first call.
+    PCIe-inclusive; first call (keys join) and the median of the next `reps`."""
+    from narwhal_amd import _lib
+    # offsets are int32 < 2^31: the same bytes as the uint32 the ABI reads
+    d, o, p, s = (np.ascontiguousarray(t.cpu().numpy()) for t in (cdig, offs, pks, sigs))
+    nv = p.shape[0]
+    cert = ctypes.create_string_buffer((m + 7) // 8)
+    badb = ctypes.create_string_buffer((nv + 7) // 8)
+    call = lambda: lib.nwc_verify_batch_many(_lib.buf(d), _lib.buf(o), _lib.buf(p), _lib.buf(s), m, cert, badb)  # noqa: E731
+    t0 = time.perf_counter()
+    _lib.check(call())
+    first = time.perf_counter() - t0
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _lib.check(call())
+        ts.append(time.perf_counter() - t0)
+    med = sorted(ts)[len(ts) // 2]
+    want_bad = bad.cpu().numpy()
+    got_bad = np.unpackbits(np.frombuffer(badb.raw, np.uint8), bitorder="little")[:nv].astype(bool)
+    got_cert = np.unpackbits(np.frombuffer(cert.raw, np.uint8), bitorder="little")[:m].astype(bool)
+    ok = bool((got_bad == want_bad).all() and (got_cert == ~want_bad.reshape(m, Q).any(axis=1)).all())
+    h = ctypes.c_uint32()
+    _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
+    return {"workload": "cfg3 from pageable host buffers through nwc_verify_batch_many (H2D + verify + D2H), "
+                        "no nwc_set_committee", "votes_per_s": nv / med, "ms_per_call": med * 1e3,
+            "first_call_ms": first * 1e3, "reps": reps, "parity_ok": ok, "launch_keys_held": h.value}
 
 
 def make_cfg3_wire(m: int, N: int = 100, Q: int = 67):

@@ -6,6 +6,11 @@ and compared verdict by verdict with the CPU restatement (oracle/, multithreaded
 
     python tests/soak.py [--n 8388608] [--chunk 1048576] [--committee K] [--call C] [--straus] [--out gpurun_out/soak.json]
 
+--launch-keys K draws the signers from K keys WITHOUT registering them: every chunk's batch-leaf
+launch (>= 65,536 equations) detects its repeated keys itself (launch keys) -- the
+committee's, the small-order encodings and the golden cases' keys mutate() tiles in -- and decides
+their votes with the comb kernel, the rest with the ladder.
+
 --call C verifies each chunk in device calls of at most C equations (C <= 1024 without a
 committee: the cold kernel, k_verify_cold, one block per equation).
 --straus also runs every chunk through dalek's batch equation over sub-batches
@@ -84,12 +89,17 @@ def main():
     ap.add_argument("--committee", type=int, default=0,
                     help="K > 0: signers drawn from K keys registered with nwc_set_committee (comb path, "
                          "cached ladder and the uncached list for mutated keys)")
+    ap.add_argument("--launch-keys", type=int, default=0,
+                    help="K > 0: signers drawn from K keys that are NOT registered (launch keys)")
     ap.add_argument("--call", type=int, default=0, help="C > 0: device calls of at most C equations")
     ap.add_argument("--straus", action="store_true", help="also the Straus sub-batch path (per-vote bits vs the oracle)")
     ap.add_argument("--valid-frac", type=float, default=0.30,
                     help="share of unmutated triples (0.99: most Straus sub-batches pass, the rest exercise the leaves)")
     args = ap.parse_args()
     lib = _lib.load()
+    _lib.check(lib.nwc_set_committee(None, 0))
+    if args.launch_keys:
+        lseeds = device.derive32(b"soak-lk-seed", 0, args.launch_keys)
     if args.committee:
         cseeds = device.derive32(b"soak-seed", 0, args.committee)
         cpks, _ = device.keygen_sign(cseeds, cseeds)
@@ -112,6 +122,9 @@ def main():
         if args.committee:
             who = torch.from_numpy(rng.integers(0, args.committee, n)).cuda()
             seeds = cseeds[who]
+        elif args.launch_keys:
+            who = torch.from_numpy(rng.integers(0, args.launch_keys, n)).cuda()
+            seeds = lseeds[who]
         else:
             seeds = device.derive32(b"soak-seed", done, n)
         msgs = device.derive32(b"soak-msg", done, n)
@@ -157,7 +170,14 @@ def main():
         print("soak %d / %d  %.0f s" % (done, args.n, time.time() - t0), file=sys.stderr, flush=True)
     total = {k: sum(v[k] for v in stats.values()) for k in ("n", "strict_mismatch", "leaf_mismatch", "straus_mismatch",
                                                              "randomized", "straus_randomized_pass")}
-    out = {"triples": args.n, "committee": args.committee, "call": args.call, "straus": args.straus,
+    held = None
+    if args.launch_keys:
+        import ctypes
+        h = ctypes.c_uint32()
+        _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
+        held = h.value
+    out = {"triples": args.n, "committee": args.committee, "launch_keys": args.launch_keys, "launch_keys_held": held,
+           "call": args.call, "straus": args.straus,
            "valid_frac": args.valid_frac, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
            "mismatches": mism}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
