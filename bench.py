@@ -61,7 +61,7 @@ CFG4_BATCH_BYTES = 12 + CFG4_TXS * (8 + CFG4_TX_BYTES)   # 508,052
 CFG4_STRIDE = (CFG4_BATCH_BYTES + 255) & ~255
 
 
-PROFILE_ROUND = "r03"   # profiles/<round>/summary.json: rocprofv3 PMC passes of this build
+PROFILE_ROUND = "r04"   # profiles/<round>/summary.json: rocprofv3 PMC passes of this build
 
 
 def profile_counters(*kernel_names: str):
