@@ -23,66 +23,9 @@
 #pragma once
 #include <array>
 #include <atomic>
-#include <functional>
-#include <condition_variable>
 #include <deque>
 
 namespace {
-
-// A fixed set of host threads that fill one pinned stage together (each a contiguous byte range):
-// one memcpy thread moves ~30 GB/s, and spawning threads per 32-MB stage costs ~10 % of the fill.
-struct CopyPool {
-  std::vector<std::thread> th;
-  std::mutex m;
-  std::condition_variable cv, cv_done;
-  uint64_t gen = 0;
-  unsigned used = 0, pending = 0;
-  bool quit = false;
-  std::function<void(unsigned)> job;
-  void start(unsigned n) {   // n - 1 helpers; the caller is part 0
-    for (unsigned i = 1; i < n; ++i)
-      th.emplace_back([this, i] {
-        uint64_t seen = 0;
-        for (;;) {
-          std::unique_lock<std::mutex> lk(m);
-          cv.wait(lk, [&] { return quit || gen != seen; });
-          if (quit) return;
-          seen = gen;
-          if (i >= used) continue;
-          auto f = job;
-          lk.unlock();
-          f(i);
-          lk.lock();
-          if (--pending == 0) cv_done.notify_one();
-        }
-      });
-  }
-  // f(0 .. parts-1), part 0 on the calling thread
-  void run(unsigned parts, const std::function<void(unsigned)>& f) {
-    parts = std::min<unsigned>(parts, (unsigned)th.size() + 1);
-    if (parts <= 1) { f(0); return; }
-    {
-      std::lock_guard<std::mutex> lk(m);
-      job = f;
-      used = parts;
-      pending = parts - 1;
-      ++gen;
-    }
-    cv.notify_all();
-    f(0);
-    std::unique_lock<std::mutex> lk(m);
-    cv_done.wait(lk, [&] { return pending == 0; });
-  }
-  void stop() {
-    {
-      std::lock_guard<std::mutex> lk(m);
-      quit = true;
-    }
-    cv.notify_all();
-    for (auto& t : th) t.join();
-    th.clear();
-  }
-};
 
 struct Digester {
   struct Item { const uint8_t* p; size_t len; uint64_t tag; int status = 0; };

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "nwc.h"
+#include "copy_pool.h"
 #include "kernels.hip"
 #include "launch_keys.h"
 #include "messages.h"
@@ -182,6 +183,8 @@ struct DevCtx {
   // launch keys (launch_keys.h): allocated by the first large batch-leaf launch without a committee
   nwc::LaunchKeys lk{};
   bool lk_alloc = false;
+  // large host calls: pageable inputs through pinned stages on `xfer` (created on first use)
+  std::unique_ptr<HostStager> stager;
   std::mutex mu;
 
   int ensure_pinned(size_t bytes) {
@@ -647,6 +650,23 @@ int lk_ensure(DevCtx& d, hipStream_t s) {
   return 0;
 }
 
+// NWC_HOST_STAGING=0: large host calls copy straight from pageable memory (A/B); otherwise through
+// the device's pinned stages, filled by NWC_HOST_STAGING_THREADS (8) host threads.
+bool host_staging() {
+  static const bool on = [] {
+    const char* e = std::getenv("NWC_HOST_STAGING");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+unsigned stager_threads() {
+  static const unsigned t = [] {
+    const char* e = std::getenv("NWC_HOST_STAGING_THREADS");
+    return e ? (unsigned)std::max(1, std::atoi(e)) : 8u;
+  }();
+  return t;
+}
+
 // launch_verify flags: the caller checked on the host that every key is in the committee cache,
 // and/or out_words is already zero (both let the latency path run as a single kernel)
 constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4;   // LV_AUTO: the keys are in the auto cache
@@ -1003,6 +1023,21 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     // chunk k verifies (~100 M/s), so it arrives in time while growing up to ~3.7x; fewer, larger
     // launches leave fewer kernel tails (the first chunk is one round of resident lanes).
     if (!d.xfer) HIP_TRY(hipStreamCreateWithFlags(&d.xfer, hipStreamNonBlocking));
+    if (!d.stager && host_staging()) {
+      auto st = std::make_unique<HostStager>();
+      const hipError_t e = st->init(d.xfer, stager_threads());
+      if (e != hipSuccess) {
+        st->release();
+        return set_err(NWC_ERR_DEVICE, "host stager: %s", hipGetErrorString(e));
+      }
+      d.stager = std::move(st);
+    }
+    // copies of one chunk's inputs: through the pinned stages, or straight from pageable memory
+    HostStager* const hs = host_staging() ? d.stager.get() : nullptr;
+    auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+      if (hs) return hs->put(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), bytes);
+      return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d.xfer);
+    };
     std::vector<uint64_t> cuts{0};
     for (uint64_t len = chunk; cuts.back() < n; len *= growth) {
       uint64_t next = std::min<uint64_t>(n, cuts.back() + len);
@@ -1018,14 +1053,15 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     // the previous call's kernels may still read the arena: the transfers wait for the stream
     HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
     HIP_TRY(hipStreamWaitEvent(d.xfer, d.ev_fork, 0));
-    if (msg_index) HIP_TRY(hipMemcpyAsync(dm, msgs, msg_bytes, hipMemcpyHostToDevice, d.xfer));
-    else if (!msg_stride) HIP_TRY(hipMemcpyAsync(dm, msgs, 32, hipMemcpyHostToDevice, d.xfer));
+    if (msg_index) HIP_TRY(h2d(dm, msgs, msg_bytes));
+    else if (!msg_stride) HIP_TRY(h2d(dm, msgs, 32));
     for (uint64_t k = 0; k < nch; ++k) {
       const uint64_t c0 = cuts[k], len = cuts[k + 1] - cuts[k];
-      if (msg_index) HIP_TRY(hipMemcpyAsync(dmi + c0, msg_index + lo + c0, 4 * len, hipMemcpyHostToDevice, d.xfer));
-      else if (msg_stride) HIP_TRY(hipMemcpyAsync(dm + 32 * c0, msgs + 32 * (lo + c0), 32 * len, hipMemcpyHostToDevice, d.xfer));
-      HIP_TRY(hipMemcpyAsync(dp + 32 * c0, pks + 32 * (lo + c0), 32 * len, hipMemcpyHostToDevice, d.xfer));
-      HIP_TRY(hipMemcpyAsync(ds + 64 * c0, sigs + 64 * (lo + c0), 64 * len, hipMemcpyHostToDevice, d.xfer));
+      if (msg_index) HIP_TRY(h2d(dmi + c0, msg_index + lo + c0, 4 * len));
+      else if (msg_stride) HIP_TRY(h2d(dm + 32 * c0, msgs + 32 * (lo + c0), 32 * len));
+      HIP_TRY(h2d(dp + 32 * c0, pks + 32 * (lo + c0), 32 * len));
+      HIP_TRY(h2d(ds + 64 * c0, sigs + 64 * (lo + c0), 64 * len));
+      if (hs) HIP_TRY(hs->flush());
       HIP_TRY(hipEventRecord(d.ev_chunk[k], d.xfer));
       HIP_TRY(hipStreamWaitEvent(d.stream, d.ev_chunk[k], 0));
       if (int rc = launch_verify(d, msg_stride ? dm + 32 * c0 : dm, msg_index ? dmi + c0 : nullptr, msg_stride ? 1 : 0,
@@ -1299,6 +1335,8 @@ void nwc_shutdown(void) {
     if (d->ev_join) (void)hipEventDestroy(d->ev_join);
     if (d->side) (void)hipStreamDestroy(d->side);
     if (d->xfer) (void)hipStreamSynchronize(d->xfer);
+    if (d->stager) d->stager->release();
+    d->stager.reset();
     for (hipEvent_t e : d->ev_chunk) (void)hipEventDestroy(e);
     if (d->xfer) (void)hipStreamDestroy(d->xfer);
     if (d->stream) (void)hipStreamDestroy(d->stream);
