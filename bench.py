@@ -87,6 +87,14 @@ def ops_per_verify() -> float:
 
 
 # ---- distributed ---------------------------------------------------------------------------
+def progress(msg: str) -> None:
+    """One line per bench leg on stderr (the JSON line stays alone on stdout)."""
+    print("[bench %.0f s] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+
+
 def dist_setup(args):
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -377,6 +385,7 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
             ("clean_no_cache_straus", False, "straus", clean_pks, clean_sigs, no_bad),
             ("launch_keys", False, "launch", pks, sigs, bad), ("cache", True, "leaf", pks, sigs, bad))
     for tag, use_cache, eq, P, S, want_bad in legs:
+        progress("config 3: " + tag)
         _lib.check(lib.nwc_set_committee(None, 0))   # no committee cache, launch keys emptied
         _lib.diag_set("launch_keys", 1 if eq == "launch" else 0)
         if use_cache:
@@ -913,6 +922,7 @@ def main():
     lib = _lib.load(device_mask=1 << local)   # the library drives the same GPU as this rank
 
     # ---------------- verify leg (headline)
+    progress("headline: config 2 verify")
     n = args.n
     msgs, pks, sigs = make_cfg2(rank, n)
     words = torch.empty(device.words_for(n), dtype=torch.int64, device="cuda")
@@ -949,6 +959,7 @@ def main():
     # ---------------- digest leg (cfg 4)
     digest = None
     if args.digest_batches > 0:
+        progress("config 4 digest")
         pool = min(args.digest_pool, args.digest_batches)
         data = make_cfg4_pool(pool)
         nb = args.digest_batches
@@ -983,6 +994,7 @@ def main():
                   "effective_valu_frac": dk_gbs * 1e9 / 128 * OPS_SHA / (VALU_PEAK_TOPS * 1e12)}
 
     extras = {}
+    progress("extra configurations")
     if world == 1 and args.e2e_reps > 0:
         extras["cfg2_host_abi"] = bench_cfg2_host_abi(lib, msgs, pks, sigs, args.e2e_reps)
     if world == 1 and args.e2e_reps > 0 and args.host_digest_group > 0:
@@ -1002,6 +1014,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
+        progress("CPU baselines")
         cpu = cpu_baseline_verify(msgs, pks, sigs, args.cpu_budget)
         if digest is not None:
             digest["cpu_baseline"] = cpu_baseline_digest(args.cpu_budget / 2)

@@ -66,6 +66,9 @@ struct CopyPool {
     for (auto& t : th) t.join();
     th.clear();
   }
+  // a pool still running at process exit (its owner's context was never shut down) is stopped
+  // here: destroying a joinable std::thread would call std::terminate
+  ~CopyPool() { stop(); }
 };
 
 // Pageable host arrays into device memory at the pinned-DMA rate.  hipMemcpyAsync from pageable
@@ -86,6 +89,10 @@ struct HostStager {
   size_t fill = 0;
   std::vector<Seg> segs;
   hipStream_t stream = nullptr;
+
+  // At process exit without nwc_shutdown the pool's threads are stopped (CopyPool's destructor);
+  // the pinned stages are left to the process teardown (the HIP runtime may be gone by then).
+  ~HostStager() = default;
 
   hipError_t init(hipStream_t s, unsigned threads) {
     stream = s;

@@ -667,6 +667,21 @@ unsigned stager_threads() {
   return t;
 }
 
+// The device's transfer stream and (NWC_HOST_STAGING) its pinned stages.  Caller holds d.mu.
+int ensure_stager(DevCtx& d) {
+  if (!d.xfer) HIP_TRY(hipStreamCreateWithFlags(&d.xfer, hipStreamNonBlocking));
+  if (!d.stager && host_staging()) {
+    auto st = std::make_unique<HostStager>();
+    const hipError_t e = st->init(d.xfer, stager_threads());
+    if (e != hipSuccess) {
+      st->release();
+      return set_err(NWC_ERR_DEVICE, "host stager: %s", hipGetErrorString(e));
+    }
+    d.stager = std::move(st);
+  }
+  return 0;
+}
+
 // launch_verify flags: the caller checked on the host that every key is in the committee cache,
 // and/or out_words is already zero (both let the latency path run as a single kernel)
 constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4;   // LV_AUTO: the keys are in the auto cache
@@ -1022,16 +1037,7 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     // Chunk k + 1 is up to `growth` x chunk k: its 128 B per equation cross PCIe (~50 GB/s) while
     // chunk k verifies (~100 M/s), so it arrives in time while growing up to ~3.7x; fewer, larger
     // launches leave fewer kernel tails (the first chunk is one round of resident lanes).
-    if (!d.xfer) HIP_TRY(hipStreamCreateWithFlags(&d.xfer, hipStreamNonBlocking));
-    if (!d.stager && host_staging()) {
-      auto st = std::make_unique<HostStager>();
-      const hipError_t e = st->init(d.xfer, stager_threads());
-      if (e != hipSuccess) {
-        st->release();
-        return set_err(NWC_ERR_DEVICE, "host stager: %s", hipGetErrorString(e));
-      }
-      d.stager = std::move(st);
-    }
+    if (int rc = ensure_stager(d)) return rc;
     // copies of one chunk's inputs: through the pinned stages, or straight from pageable memory
     HostStager* const hs = host_staging() ? d.stager.get() : nullptr;
     auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
@@ -1870,7 +1876,19 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
   uint8_t* ddig = digests32 ? c.take<uint8_t>(32 * m) : nullptr;
   std::vector<uint64_t> hoff(m + 1);
   for (size_t i = 0; i <= m; ++i) hoff[i] = offsets[i] - base;
-  HIP_TRY(hipMemcpyAsync(ddata, data + base, total, hipMemcpyHostToDevice, d.stream));
+  if (host_staging() && total >= ((size_t)4 << 20)) {
+    // large batches (config 3 from the wire: 10 KB per certificate) through the pinned stages on
+    // the transfer stream, after every launch that may still read the arena
+    if (int rc = ensure_stager(d)) return rc;
+    HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
+    HIP_TRY(hipStreamWaitEvent(d.xfer, d.ev_fork, 0));
+    HIP_TRY(d.stager->put(ddata, data + base, total));
+    HIP_TRY(d.stager->flush());
+    HIP_TRY(hipEventRecord(d.ev_fork, d.xfer));
+    HIP_TRY(hipStreamWaitEvent(d.stream, d.ev_fork, 0));
+  } else {
+    HIP_TRY(hipMemcpyAsync(ddata, data + base, total, hipMemcpyHostToDevice, d.stream));
+  }
   HIP_TRY(hipMemsetAsync(ddata + total, 0, 16, d.stream));
   HIP_TRY(hipMemcpyAsync(doff, hoff.data(), 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
   if (int rc = sanitize_dev(d, ddata, doff, m, total, gc_round, vote_target, dcodes, ddig, drec, d.stream)) return rc;

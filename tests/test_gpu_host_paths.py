@@ -60,3 +60,66 @@ def test_batch_many_host_chunks(oracle):
     _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
     assert h.value == N
     _lib.check(lib.nwc_set_committee(None, 0))
+
+
+def test_sanitize_messages_host_staged():
+    """nwc_sanitize_messages on a batch above the staging threshold (4 MB of wire bytes, through the
+    pinned stages): the golden wire fixtures tiled ~500 times, every code and digest as the fixture
+    says (primary/src/core.rs:306-346 via the restatement, tests/golden/messages.json)."""
+    import json
+    import os
+    from narwhal_amd import _lib
+    from tests.conftest import GOLDEN
+    lib = _lib.load()
+    g = json.load(open(os.path.join(GOLDEN, "messages.json")))
+    c = g["committee"]
+    n = len(c["keys"])
+    offs_w, ids = [0], []
+    for w in c["workers"]:
+        ids.extend(w)
+        offs_w.append(len(ids))
+    kb = b"".join(bytes.fromhex(k) for k in c["keys"])
+    _lib.check(lib.nwc_set_committee_config(_lib.buf(kb), (ctypes.c_uint64 * n)(*c["stakes"]), n,
+                                            (ctypes.c_uint32 * (n + 1))(*offs_w), (ctypes.c_uint32 * max(1, len(ids)))(*ids)))
+    try:
+        cases = [x for x in g["cases"] if x["gc_round"] == 0 and x["target"] is None]
+        reps = 1 + (8 << 20) // sum(len(x["msg"]) // 2 for x in cases)
+        tiled = cases * reps
+        msgs = [bytes.fromhex(x["msg"]) for x in tiled]
+        offs = np.zeros(len(msgs) + 1, np.uint64)
+        offs[1:] = np.cumsum([len(b) for b in msgs])
+        assert offs[-1] >= (4 << 20)
+        data = b"".join(msgs)
+        codes = np.zeros(len(msgs), np.int32)
+        dig = np.zeros((len(msgs), 32), np.uint8)
+        kinds = np.zeros(len(msgs), np.uint8)
+        _lib.check(lib.nwc_sanitize_messages(_lib.buf(data), _lib.buf(offs), len(msgs), 0, None, _lib.buf(codes),
+                                             _lib.buf(dig), _lib.buf(kinds)))
+        for i, x in enumerate(tiled):
+            assert codes[i] == x["code"], (i, x["name"], int(codes[i]))
+            if x["kind"] >= 0 and x["kind"] != 3:
+                assert dig[i].tobytes().hex() == x["digest"] and kinds[i] == x["kind"], (i, x["name"])
+    finally:
+        lib.nwc_set_committee(None, 0)
+
+
+def test_process_exits_after_staged_calls():
+    """A process that made staged host calls and never called nwc_shutdown (a Python or Rust caller
+    that just exits) must exit cleanly: the stager's copy threads are stopped at teardown (a
+    joinable std::thread destroyed at exit would call std::terminate)."""
+    import os
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    code = ("import ctypes, sys; sys.path.insert(0, %r)\n"
+            "import numpy as np\n"
+            "from narwhal_amd import _lib\n"
+            "lib = _lib.load()\n"
+            "n = 300000\n"
+            "z = np.zeros((n, 32), np.uint8); s = np.zeros((n, 64), np.uint8)\n"
+            "out = ctypes.create_string_buffer((n + 7) // 8)\n"
+            "_lib.check(lib.nwc_verify_strict_many(_lib.buf(z), _lib.buf(z), _lib.buf(s), n, out))\n"
+            "print('done', flush=True)\n" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, cwd=ROOT,
+                       env=dict(os.environ))
+    assert r.returncode == 0 and "done" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-2000:])
