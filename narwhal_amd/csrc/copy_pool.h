@@ -113,6 +113,11 @@ struct HostStager {
       ev[k] = nullptr;
     }
   }
+  // drop copies queued by a call that failed before its flush (their sources are gone)
+  void reset() {
+    fill = 0;
+    segs.clear();
+  }
   hipError_t put(uint8_t* dst, const uint8_t* src, size_t len) {
     while (len) {
       if (fill == STAGE)

@@ -1040,6 +1040,7 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     if (int rc = ensure_stager(d)) return rc;
     // copies of one chunk's inputs: through the pinned stages, or straight from pageable memory
     HostStager* const hs = host_staging() ? d.stager.get() : nullptr;
+    if (hs) hs->reset();
     auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
       if (hs) return hs->put(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), bytes);
       return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d.xfer);
@@ -1882,6 +1883,7 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
     if (int rc = ensure_stager(d)) return rc;
     HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
     HIP_TRY(hipStreamWaitEvent(d.xfer, d.ev_fork, 0));
+    d.stager->reset();
     HIP_TRY(d.stager->put(ddata, data + base, total));
     HIP_TRY(d.stager->flush());
     HIP_TRY(hipEventRecord(d.ev_fork, d.xfer));

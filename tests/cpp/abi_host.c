@@ -27,6 +27,9 @@
  *                                          malloc'd buffers, or written into its receive arena),
  *                                          polled until every tag is back; the batches and their
  *                                          digests are kept for Y
+ *   W <k>                               -> "W <mismatches>": the last V request tiled k times through
+ *                                          nwc_verify_strict_many (large enough for the pipelined
+ *                                          chunks and the pinned host stages), bits vs V's
  *   Y <verify threads> <rounds>         -> "Y <mismatches>": one thread streams the last G's
  *                                          batches through a new digester `rounds` times while
  *                                          the verify threads re-run every B request and the
@@ -479,6 +482,29 @@ int main(void) {
       free(tags);
       free(dig);
       printf("G %d\n", nwc_digester_destroy(q));
+    } else if (tok[0] == 'W') {
+      const char* t = strtok(NULL, " \n");
+      if (!t || !g_vn) return 3;
+      const size_t k = (size_t)strtoul(t, NULL, 10), n = g_vn * k;
+      unsigned char* ms = malloc(32 * n + 1);
+      unsigned char* ps = malloc(32 * n + 1);
+      unsigned char* ss = malloc(64 * n + 1);
+      unsigned char* bits = calloc(n / 8 + 1, 1);
+      for (size_t j = 0; j < k; ++j) {
+        memcpy(ms + 32 * g_vn * j, g_vm, 32 * g_vn);
+        memcpy(ps + 32 * g_vn * j, g_vp, 32 * g_vn);
+        memcpy(ss + 64 * g_vn * j, g_vs, 64 * g_vn);
+      }
+      long mism = nwc_verify_strict_many(ms, ps, ss, n, bits) != 0 ? 1000000 : 0;
+      for (size_t i = 0; i < n; ++i) {
+        const size_t v = i % g_vn;
+        mism += ((bits[i >> 3] >> (i & 7)) & 1) != ((g_vbits[v >> 3] >> (v & 7)) & 1);
+      }
+      printf("W %ld\n", mism);
+      free(ms);
+      free(ps);
+      free(ss);
+      free(bits);
     } else if (tok[0] == 'Y') {
       const char* t = strtok(NULL, " \n");
       const char* r = strtok(NULL, " \n");

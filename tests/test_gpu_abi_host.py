@@ -103,6 +103,10 @@ def test_c_host_under_asan(oracle, golden_verify, golden_batch):
     lines += ["%s %s %s" % (m.tobytes().hex(), p.tobytes().hex(), s.tobytes().hex()) for m, p, s in zip(msgs, pks, sigs)]
     exp = oracle.strict_many(msgs, pks, sigs)
     want.append("V 0 " + np.packbits(exp, bitorder="little").tobytes().hex())
+    # the same triples tiled 90x (810k, 270k per virtual device): pipelined chunks, input copies
+    # through the pinned stages
+    lines.append("W 90")
+    want.append("W 0")
     # certificates: 0..40 votes each over one digest per certificate
     sizes = [int(x) for x in rng.integers(0, 41, 200)]
     offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
