@@ -898,22 +898,28 @@ int shard(uint64_t n, F fn) {
 
 // Copy `nbits` bits of device verdict words to a host bitmap starting at bit `bit0`.
 void merge_bits(uint8_t* dst, uint64_t bit0, const std::vector<uint64_t>& words, uint64_t nbits) {
-  if ((bit0 & 7) == 0) {
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(words.data());
-    const uint64_t full = nbits / 8;
-    std::memcpy(dst + bit0 / 8, src, full);
-    for (uint64_t b = full * 8; b < nbits; ++b) {
-      const uint64_t o = bit0 + b;
-      const bool v = (words[b >> 6] >> (b & 63)) & 1;
-      dst[o >> 3] = (uint8_t)((dst[o >> 3] & ~(1u << (o & 7))) | ((unsigned)v << (o & 7)));
-    }
-    return;
-  }
-  for (uint64_t b = 0; b < nbits; ++b) {
+  // dst bits [bit0, bit0 + nbits) = source bits [0, nbits); bits of dst outside the range kept
+  auto put1 = [&](uint64_t b) {
     const uint64_t o = bit0 + b;
     const bool v = (words[b >> 6] >> (b & 63)) & 1;
     dst[o >> 3] = (uint8_t)((dst[o >> 3] & ~(1u << (o & 7))) | ((unsigned)v << (o & 7)));
+  };
+  uint64_t b = 0;
+  if ((bit0 & 7) == 0) {
+    const uint64_t full = nbits / 8;
+    std::memcpy(dst + bit0 / 8, words.data(), full);
+    b = full * 8;
+  } else {
+    // head bits up to a destination byte boundary, then 8 source bits per destination byte
+    for (; b < nbits && ((bit0 + b) & 7); ++b) put1(b);
+    for (; b + 8 <= nbits; b += 8) {
+      const uint64_t w = b >> 6, sh = b & 63;
+      uint64_t v = words[w] >> sh;
+      if (sh > 56 && w + 1 < words.size()) v |= words[w + 1] << (64 - sh);
+      dst[(bit0 + b) >> 3] = (uint8_t)v;
+    }
   }
+  for (; b < nbits; ++b) put1(b);
 }
 
 // Host-memory verification of equations [lo, hi) on device di.
@@ -1152,17 +1158,31 @@ int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8
 // bad-vote bitmap (a certificate passes iff every vote's bit is set; an empty one passes).
 int batch_verdicts(const uint32_t* offsets, size_t m, const std::vector<uint64_t>& cuts,
                    const std::vector<std::vector<uint64_t>>& parts, uint8_t* cert_ok_bitmap, uint8_t* bad_vote_bitmap) {
+  // word-level: a certificate is ok iff every bit of its vote range is set (two masked words for a
+  // 67-vote certificate), and the bad-vote bitmap is the complement of the leaf bits
   const uint64_t nv = offsets[m];
-  std::vector<uint8_t> leafbytes((nv + 7) / 8 + 8, 0);
-  for (size_t i = 0; i + 1 < cuts.size(); ++i) merge_bits(leafbytes.data(), cuts[i], parts[i], cuts[i + 1] - cuts[i]);
+  std::vector<uint64_t> leafw((nv + 63) / 64 + 1, 0);
+  uint8_t* const leafbytes = reinterpret_cast<uint8_t*>(leafw.data());
+  for (size_t i = 0; i + 1 < cuts.size(); ++i) merge_bits(leafbytes, cuts[i], parts[i], cuts[i + 1] - cuts[i]);
   std::memset(cert_ok_bitmap, 0, (m + 7) / 8);
   for (size_t c = 0; c < m; ++c) {
+    const uint64_t a = offsets[c], e = offsets[c + 1];
     bool ok = true;
-    for (uint32_t v = offsets[c]; v < offsets[c + 1]; ++v) ok = ok && ((leafbytes[v >> 3] >> (v & 7)) & 1);
+    if (e > a) {
+      const uint64_t w0 = a >> 6, w1 = (e - 1) >> 6;
+      for (uint64_t w = w0; w <= w1 && ok; ++w) {
+        uint64_t mask = ~0ull;
+        if (w == w0) mask &= ~0ull << (a & 63);
+        if (w == w1) mask &= ~0ull >> (63 - ((e - 1) & 63));
+        ok = (leafw[w] & mask) == mask;
+      }
+    }
     if (ok) cert_ok_bitmap[c >> 3] |= (uint8_t)(1u << (c & 7));
   }
-  if (bad_vote_bitmap) {
-    for (uint64_t v = 0; v < nv; ++v) {
+  if (bad_vote_bitmap && nv) {
+    const uint64_t full = nv / 8;
+    for (uint64_t i = 0; i < full; ++i) bad_vote_bitmap[i] = (uint8_t)~leafbytes[i];
+    for (uint64_t v = full * 8; v < nv; ++v) {
       const bool bad = !((leafbytes[v >> 3] >> (v & 7)) & 1);
       bad_vote_bitmap[v >> 3] = (uint8_t)((bad_vote_bitmap[v >> 3] & ~(1u << (v & 7))) | ((unsigned)bad << (v & 7)));
     }
@@ -1407,9 +1427,7 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
   if (nv && (!pks || !sigs)) return set_err(NWC_ERR_ARG, "null vote buffer");
   // vote -> certificate index (host side; the kernel reads digests through it)
   std::vector<uint32_t> mi(nv);
-  for (size_t c = 0; c < m; ++c)
-    for (uint32_t v = offsets[c]; v < offsets[c + 1]; ++v) mi[v] = (uint32_t)c;
-  std::vector<uint64_t> leaf((nv + 63) / 64, 0);
+  for (size_t c = 0; c < m; ++c) std::fill(mi.begin() + offsets[c], mi.begin() + offsets[c + 1], (uint32_t)c);
   // shard votes on certificate boundaries
   const int nd = (int)g_devs.size();
   std::vector<uint64_t> cuts(nd + 1);
@@ -1438,8 +1456,7 @@ int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets
   const uint64_t nv = offsets[m];
   if (nv && (!pks || !sigs)) return set_err(NWC_ERR_ARG, "null vote buffer");
   std::vector<uint32_t> mi(nv);
-  for (size_t c = 0; c < m; ++c)
-    for (uint32_t v = offsets[c]; v < offsets[c + 1]; ++v) mi[v] = (uint32_t)c;
+  for (size_t c = 0; c < m; ++c) std::fill(mi.begin() + offsets[c], mi.begin() + offsets[c + 1], (uint32_t)c);
   const int nd = (int)g_devs.size();
   std::vector<uint64_t> cuts(nd + 1);
   nwc_cert_cuts(offsets, m, (uint32_t)nd, cuts.data());

@@ -148,14 +148,7 @@ template <bool ASM = false> __device__ __forceinline__ void sha512_compress(uint
     sha_pass_constants<ASM>(0, k);
     NWC_SHA_16ROUNDS
   }
-#ifndef NWC_SHA_UNROLL
-#define NWC_SHA_UNROLL 0
-#endif
-#if NWC_SHA_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
   for (int pass = 1; pass < 5; ++pass) {
     constexpr bool SCHED = true;
     uint64_t k[16];
