@@ -659,6 +659,11 @@ bool host_staging() {
   }();
   return on;
 }
+// NWC_HOST_TIMING: per-phase times of large host calls on stderr (diagnostics)
+bool host_timing() {
+  static const bool on = std::getenv("NWC_HOST_TIMING") != nullptr;
+  return on;
+}
 unsigned stager_threads() {
   static const unsigned t = [] {
     const char* e = std::getenv("NWC_HOST_STAGING_THREADS");
@@ -1047,6 +1052,7 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     // copies of one chunk's inputs: through the pinned stages, or straight from pageable memory
     HostStager* const hs = host_staging() ? d.stager.get() : nullptr;
     if (hs) hs->reset();
+    const auto tv0 = std::chrono::steady_clock::now();
     auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
       if (hs) return hs->put(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), bytes);
       return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d.xfer);
@@ -1081,8 +1087,13 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
                                  dp + 32 * c0, ds + 64 * c0, len, strict, dout + c0 / 64, d.stream))
         return rc;
     }
+    const auto tq = std::chrono::steady_clock::now();
     HIP_TRY(hipMemcpyAsync(out_words.data(), dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
+    if (host_timing())
+      std::fprintf(stderr, "nwc host call: %llu equations in %llu chunks: copies queued after %.2f ms, done %.2f ms later\n",
+                   (unsigned long long)n, (unsigned long long)nch, std::chrono::duration<double>(tq - tv0).count() * 1e3,
+                   std::chrono::duration<double>(std::chrono::steady_clock::now() - tq).count() * 1e3);
     return 0;
   }
   if (msg_index) {
@@ -1426,8 +1437,11 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
   const uint64_t nv = offsets[m];
   if (nv && (!pks || !sigs)) return set_err(NWC_ERR_ARG, "null vote buffer");
   // vote -> certificate index (host side; the kernel reads digests through it)
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
   std::vector<uint32_t> mi(nv);
   for (size_t c = 0; c < m; ++c) std::fill(mi.begin() + offsets[c], mi.begin() + offsets[c + 1], (uint32_t)c);
+  const auto t1 = clk::now();
   // shard votes on certificate boundaries
   const int nd = (int)g_devs.size();
   std::vector<uint64_t> cuts(nd + 1);
@@ -1442,7 +1456,14 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
   }
   for (auto& t : th) t.join();
   for (int r : rc) if (r < 0) return r;
-  return batch_verdicts(offsets, m, cuts, parts, cert_ok_bitmap, bad_vote_bitmap);
+  const auto t2 = clk::now();
+  const int r = batch_verdicts(offsets, m, cuts, parts, cert_ok_bitmap, bad_vote_bitmap);
+  if (host_timing()) {
+    auto ms = [](clk::duration d) { return std::chrono::duration<double>(d).count() * 1e3; };
+    std::fprintf(stderr, "nwc_verify_batch_many: %zu certificates, %llu votes: vote index %.2f ms, devices %.2f ms, verdicts %.2f ms\n",
+                 m, (unsigned long long)nv, ms(t1 - t0), ms(t2 - t1), ms(clk::now() - t2));
+  }
+  return r;
 }
 
 int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
