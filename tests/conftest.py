@@ -37,3 +37,15 @@ def golden_sha():
 def oracle():
     from tests.oracle_lib import load_oracle
     return load_oracle()
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """Name the library this session tested: the build id libnwc.so embeds and the hash of the
+    sources in this tree (narwhal_amd/build.py), so the run's output proves which binary ran."""
+    try:
+        from narwhal_amd import build
+        lib_id = build.embedded_id()
+        terminalreporter.write_line("libnwc.so build id %s; sources in this tree %s%s" % (
+            lib_id, build.source_id(), "" if lib_id == build.source_id() else "  (MISMATCH: stale library)"))
+    except Exception as e:  # noqa: BLE001
+        terminalreporter.write_line("libnwc.so build id unavailable: %r" % (e,))
