@@ -223,6 +223,9 @@ struct DevCtx {
 #ifndef NWC_HOST_CHUNK
 #define NWC_HOST_CHUNK (1u << 17)
 #endif
+#ifndef NWC_HOST_CHUNK_MAX
+#define NWC_HOST_CHUNK_MAX (1u << 20)
+#endif
 #ifndef NWC_HOST_CHUNK_GROWTH
 #define NWC_HOST_CHUNK_GROWTH 3
 #endif
@@ -1058,7 +1061,14 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
       return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d.xfer);
     };
     std::vector<uint64_t> cuts{0};
-    for (uint64_t len = chunk; cuts.back() < n; len *= growth) {
+    // chunks stop growing at NWC_HOST_CHUNK_MAX equations: when the kernels keep pace with the
+    // copies (the comb kernel: ~640 M votes/s against ~600 M votes/s of inputs through the stages)
+    // a huge last chunk would start only once all its inputs are in and run alone at the end
+    static const uint64_t chunk_max = [] {
+      const char* e = std::getenv("NWC_HOST_CHUNK_MAX");   // A/B
+      return e ? std::max<uint64_t>(64, std::strtoull(e, nullptr, 10)) : (uint64_t)NWC_HOST_CHUNK_MAX;
+    }();
+    for (uint64_t len = chunk; cuts.back() < n; len = std::min(len * growth, std::max(chunk, chunk_max))) {
       uint64_t next = std::min<uint64_t>(n, cuts.back() + len);
       if (n - next < chunk / 2) next = n;   // no sliver of a last chunk
       cuts.push_back(next);
