@@ -6,6 +6,7 @@
 //                          mode LEAF   = batch leaf, A.5           (crypto/src/lib.rs:206-219)
 //                        verdicts leave as a 64-bit ballot per wave (bit i = lane i valid)
 //   k_cert_reduce        per-certificate AND of leaf bits + bad-vote bitmap
+//   k_cert_index         vote -> certificate index of a host call's votes, from the offsets
 //   k_sha512_digest32    Sha512::digest(batch)[..32] per message (worker/src/processor.rs:38)
 //   k_keygen_sign        synthetic (pk, sig) generation (RFC 8032 == dalek sign) for workloads
 //
@@ -1941,6 +1942,19 @@ __global__ void k_cert_reduce(const uint64_t* __restrict__ leaf_bits, const uint
     const uint64_t lo = c * 64;
     if (lo + 64 > nvotes) wv &= (nvotes - lo >= 64) ? ~0ull : ((1ull << (nvotes - lo)) - 1);
     bad_bits[c] = wv;
+  }
+}
+
+// vote -> certificate index of the votes [lo, hi) of a host call (nwc_verify_batch_many): offs holds
+// the absolute vote offsets of certificates c0 .. c0 + ncert (ncert + 1 entries).  One wave per
+// certificate, its lanes over the certificate's votes (coalesced stores).
+__global__ void k_cert_index(const uint32_t* __restrict__ offs, uint32_t c0, uint32_t ncert, uint64_t lo, uint64_t hi,
+                             uint32_t* __restrict__ idx) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < ncert; w += nw) {
+    const uint64_t a = max((uint64_t)offs[w], lo), b = min((uint64_t)offs[w + 1], hi);
+    for (uint64_t v = a + lane; v < b; v += 64) idx[v - lo] = c0 + (uint32_t)w;
   }
 }
 

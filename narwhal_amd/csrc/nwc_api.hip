@@ -930,8 +930,33 @@ void merge_bits(uint8_t* dst, uint64_t bit0, const std::vector<uint64_t>& words,
   for (; b < nbits; ++b) put1(b);
 }
 
-// Host-memory verification of equations [lo, hi) on device di.
-int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_t* msg_index,
+// Certificates [c_lo, c_end) of offsets (m + 1 entries) whose votes meet [lo, hi), lo < hi <= offsets[m].
+void cert_span(const uint32_t* offsets, uint64_t m, uint64_t lo, uint64_t hi, uint64_t& c_lo, uint64_t& c_end) {
+  c_lo = (uint64_t)(std::upper_bound(offsets, offsets + m + 1, (uint32_t)lo) - offsets) - 1;   // offsets[c_lo] <= lo
+  c_end = (uint64_t)(std::lower_bound(offsets, offsets + m + 1, (uint32_t)hi) - offsets);     // first offsets[c] >= hi
+}
+
+// vote -> certificate index of votes [lo, hi) on the host (small calls; k_cert_index on the device)
+void fill_cert_index(uint32_t* dst, const uint32_t* offsets, uint64_t c_lo, uint64_t c_end, uint64_t lo, uint64_t hi) {
+  for (uint64_t c = c_lo; c < c_end; ++c) {
+    const uint64_t a = std::max<uint64_t>(offsets[c], lo), b = std::min<uint64_t>(offsets[c + 1], hi);
+    if (b > a) std::fill(dst + (a - lo), dst + (b - lo), (uint32_t)c);
+  }
+}
+
+// vote -> certificate index of votes [lo, hi) on stream s, from the offsets already at doffs
+// (certificates c_lo .. c_end)
+void launch_cert_index(const uint32_t* doffs, uint64_t c_lo, uint64_t c_end, uint64_t lo, uint64_t hi, uint32_t* dmi,
+                       hipStream_t s) {
+  const uint64_t ncert = c_end - c_lo;
+  const unsigned grid = (unsigned)std::min<uint64_t>((ncert * 64 + 255) / 256, 16384);
+  hipLaunchKernelGGL(nwc::k_cert_index, dim3(grid), dim3(256), 0, s, doffs, (uint32_t)c_lo, (uint32_t)ncert, lo, hi, dmi);
+}
+
+// Host-memory verification of equations [lo, hi) on device di.  Batch mode (cert_offsets, the m + 1
+// vote offsets of the call's certificates; msgs = their m digests): equation v checks digest c with
+// offsets[c] <= v < offsets[c + 1], the index built on the device for large ranges.
+int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_t* cert_offsets,
                  const uint8_t* pks, const uint8_t* sigs, uint64_t lo, uint64_t hi, int strict,
                  std::vector<uint64_t>& out_words, uint64_t nmsgs) {
   DevCtx& d = *ctx(di);
@@ -941,22 +966,27 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
   const uint64_t words = (n + 63) / 64;
   out_words.assign(words, 0);
   if (n == 0) return 0;
-  const uint64_t msg_bytes = msg_index ? 32 * nmsgs : (msg_stride ? 32 * n : 32);
-  const size_t need = align256(msg_bytes) + align256(msg_index ? 4 * n : 0) + align256(32 * n) + align256(64 * n) +
+  const bool batch = cert_offsets != nullptr;
+  uint64_t c_lo = 0, c_end = 0;
+  if (batch) cert_span(cert_offsets, nmsgs, lo, hi, c_lo, c_end);
+  const uint64_t msg_bytes = batch ? 32 * nmsgs : (msg_stride ? 32 * n : 32);
+  const size_t need = align256(msg_bytes) + align256(batch ? 4 * n : 0) + align256(32 * n) + align256(64 * n) +
                       align256(8 * (words + 1));
-  if (int rc = d.ensure_arena(need)) return rc;
+  const size_t offs_bytes = batch ? 4 * (c_end - c_lo + 1) : 0;
+  if (int rc = d.ensure_arena(need + align256(offs_bytes))) return rc;
   Carve c(d.arena);
   uint8_t* dm = c.take<uint8_t>(msg_bytes);
-  uint32_t* dmi = msg_index ? c.take<uint32_t>(4 * n) : nullptr;
+  uint32_t* dmi = batch ? c.take<uint32_t>(4 * n) : nullptr;
   uint8_t* dp = c.take<uint8_t>(32 * n);
   uint8_t* ds = c.take<uint8_t>(64 * n);
   uint64_t* dout = c.take<uint64_t>(8 * (words + 1));   // + the latency kernel's missing-key word
+  uint32_t* doffs = batch ? c.take<uint32_t>(offs_bytes) : nullptr;   // large ranges: k_cert_index's input
   if (need <= NWC_PINNED_STAGE_MAX) {
     // small call (a certificate, a header): pack into pinned memory, one H2D, one D2H
     if (int rc = d.ensure_pinned(NWC_PINNED_STAGE_MAX)) return rc;
     uint8_t* h = d.pinned;
-    std::memcpy(h + (dm - d.arena), msg_index ? msgs : msgs + (msg_stride ? 32 * lo : 0), msg_bytes);
-    if (msg_index) std::memcpy(h + ((uint8_t*)dmi - d.arena), msg_index + lo, 4 * n);
+    std::memcpy(h + (dm - d.arena), batch ? msgs : msgs + (msg_stride ? 32 * lo : 0), msg_bytes);
+    if (batch) fill_cert_index(reinterpret_cast<uint32_t*>(h + ((uint8_t*)dmi - d.arena)), cert_offsets, c_lo, c_end, lo, hi);
     std::memcpy(h + (dp - d.arena), pks + 32 * lo, 32 * n);
     std::memcpy(h + (ds - d.arena), sigs + 64 * lo, 64 * n);
     std::memset(h + ((uint8_t*)dout - d.arena), 0, 8 * (words + 1));
@@ -1082,18 +1112,26 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     // the previous call's kernels may still read the arena: the transfers wait for the stream
     HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
     HIP_TRY(hipStreamWaitEvent(d.xfer, d.ev_fork, 0));
-    if (msg_index) HIP_TRY(h2d(dm, msgs, msg_bytes));
-    else if (!msg_stride) HIP_TRY(h2d(dm, msgs, 32));
+    if (batch) {
+      // digests and offsets first; the vote index is built on the device behind them, so chunk 0's
+      // event (recorded later on the same stream) covers it
+      HIP_TRY(h2d(dm, msgs, msg_bytes));
+      HIP_TRY(h2d(doffs, cert_offsets + c_lo, offs_bytes));
+      if (hs) HIP_TRY(hs->flush());
+      launch_cert_index(doffs, c_lo, c_end, lo, hi, dmi, d.xfer);
+      HIP_TRY(hipGetLastError());
+    } else if (!msg_stride) {
+      HIP_TRY(h2d(dm, msgs, 32));
+    }
     for (uint64_t k = 0; k < nch; ++k) {
       const uint64_t c0 = cuts[k], len = cuts[k + 1] - cuts[k];
-      if (msg_index) HIP_TRY(h2d(dmi + c0, msg_index + lo + c0, 4 * len));
-      else if (msg_stride) HIP_TRY(h2d(dm + 32 * c0, msgs + 32 * (lo + c0), 32 * len));
+      if (msg_stride) HIP_TRY(h2d(dm + 32 * c0, msgs + 32 * (lo + c0), 32 * len));
       HIP_TRY(h2d(dp + 32 * c0, pks + 32 * (lo + c0), 32 * len));
       HIP_TRY(h2d(ds + 64 * c0, sigs + 64 * (lo + c0), 64 * len));
       if (hs) HIP_TRY(hs->flush());
       HIP_TRY(hipEventRecord(d.ev_chunk[k], d.xfer));
       HIP_TRY(hipStreamWaitEvent(d.stream, d.ev_chunk[k], 0));
-      if (int rc = launch_verify(d, msg_stride ? dm + 32 * c0 : dm, msg_index ? dmi + c0 : nullptr, msg_stride ? 1 : 0,
+      if (int rc = launch_verify(d, msg_stride ? dm + 32 * c0 : dm, batch ? dmi + c0 : nullptr, msg_stride ? 1 : 0,
                                  dp + 32 * c0, ds + 64 * c0, len, strict, dout + c0 / 64, d.stream))
         return rc;
     }
@@ -1106,9 +1144,11 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
                    std::chrono::duration<double>(std::chrono::steady_clock::now() - tq).count() * 1e3);
     return 0;
   }
-  if (msg_index) {
+  if (batch) {
     HIP_TRY(hipMemcpyAsync(dm, msgs, msg_bytes, hipMemcpyHostToDevice, d.stream));
-    HIP_TRY(hipMemcpyAsync(dmi, msg_index + lo, 4 * n, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(doffs, cert_offsets + c_lo, offs_bytes, hipMemcpyHostToDevice, d.stream));
+    launch_cert_index(doffs, c_lo, c_end, lo, hi, dmi, d.stream);
+    HIP_TRY(hipGetLastError());
   } else {
     HIP_TRY(hipMemcpyAsync(dm, msgs + (msg_stride ? 32 * lo : 0), msg_bytes, hipMemcpyHostToDevice, d.stream));
   }
@@ -1213,7 +1253,7 @@ int batch_verdicts(const uint32_t* offsets, size_t m, const std::vector<uint64_t
 
 // One device's share of nwc_verify_batch_straus_many: votes [lo, hi) (whole certificates) staged
 // into the arena with one H2D each, the Straus launch, one D2H of the leaf words.
-int straus_range(int di, const uint8_t* digests, size_t m, const uint32_t* msg_index, const uint8_t* pks,
+int straus_range(int di, const uint8_t* digests, size_t m, const uint32_t* offsets, const uint8_t* pks,
                  const uint8_t* sigs, uint64_t lo, uint64_t hi, std::vector<uint64_t>& out_words) {
   DevCtx& d = *ctx(di);
   std::lock_guard<std::mutex> lk(d.mu);
@@ -1222,7 +1262,11 @@ int straus_range(int di, const uint8_t* digests, size_t m, const uint32_t* msg_i
   const uint64_t words = (n + 63) / 64;
   out_words.assign(words, 0);
   if (n == 0) return 0;
-  const size_t need = align256(32 * m) + align256(4 * n) + align256(32 * n) + align256(64 * n) + align256(8 * words);
+  uint64_t c_lo, c_end;
+  cert_span(offsets, m, lo, hi, c_lo, c_end);
+  const size_t offs_bytes = 4 * (c_end - c_lo + 1);
+  const size_t need = align256(32 * m) + align256(4 * n) + align256(32 * n) + align256(64 * n) + align256(8 * words) +
+                      align256(offs_bytes);
   if (int rc = d.ensure_arena(need)) return rc;
   Carve c(d.arena);
   uint8_t* dm = c.take<uint8_t>(32 * m);
@@ -1230,8 +1274,11 @@ int straus_range(int di, const uint8_t* digests, size_t m, const uint32_t* msg_i
   uint8_t* dp = c.take<uint8_t>(32 * n);
   uint8_t* ds = c.take<uint8_t>(64 * n);
   uint64_t* dout = c.take<uint64_t>(8 * words);
+  uint32_t* doffs = c.take<uint32_t>(offs_bytes);
   HIP_TRY(hipMemcpyAsync(dm, digests, 32 * m, hipMemcpyHostToDevice, d.stream));
-  HIP_TRY(hipMemcpyAsync(dmi, msg_index + lo, 4 * n, hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(hipMemcpyAsync(doffs, offsets + c_lo, offs_bytes, hipMemcpyHostToDevice, d.stream));
+  launch_cert_index(doffs, c_lo, c_end, lo, hi, dmi, d.stream);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(dp, pks + 32 * lo, 32 * n, hipMemcpyHostToDevice, d.stream));
   HIP_TRY(hipMemcpyAsync(ds, sigs + 64 * lo, 64 * n, hipMemcpyHostToDevice, d.stream));
   if (int rc = launch_straus(d, dm, dmi, dp, ds, n, dout, d.stream)) return rc;
@@ -1446,11 +1493,8 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
     if (offsets[c + 1] < offsets[c]) return set_err(NWC_ERR_ARG, "offsets not monotone at %zu", c);
   const uint64_t nv = offsets[m];
   if (nv && (!pks || !sigs)) return set_err(NWC_ERR_ARG, "null vote buffer");
-  // vote -> certificate index (host side; the kernel reads digests through it)
+  // the vote -> certificate index is built per device range (k_cert_index; on the host for small calls)
   using clk = std::chrono::steady_clock;
-  const auto t0 = clk::now();
-  std::vector<uint32_t> mi(nv);
-  for (size_t c = 0; c < m; ++c) std::fill(mi.begin() + offsets[c], mi.begin() + offsets[c + 1], (uint32_t)c);
   const auto t1 = clk::now();
   // shard votes on certificate boundaries
   const int nd = (int)g_devs.size();
@@ -1461,7 +1505,7 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
   std::vector<std::thread> th;
   for (int i = 0; i < nd; ++i) {
     th.emplace_back([&, i] {
-      rc[i] = verify_range(i, digests, 0, mi.data(), pks, sigs, cuts[i], cuts[i + 1], 0, parts[i], m);
+      rc[i] = verify_range(i, digests, 0, offsets, pks, sigs, cuts[i], cuts[i + 1], 0, parts[i], m);
     });
   }
   for (auto& t : th) t.join();
@@ -1470,8 +1514,8 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
   const int r = batch_verdicts(offsets, m, cuts, parts, cert_ok_bitmap, bad_vote_bitmap);
   if (host_timing()) {
     auto ms = [](clk::duration d) { return std::chrono::duration<double>(d).count() * 1e3; };
-    std::fprintf(stderr, "nwc_verify_batch_many: %zu certificates, %llu votes: vote index %.2f ms, devices %.2f ms, verdicts %.2f ms\n",
-                 m, (unsigned long long)nv, ms(t1 - t0), ms(t2 - t1), ms(clk::now() - t2));
+    std::fprintf(stderr, "nwc_verify_batch_many: %zu certificates, %llu votes: devices %.2f ms, verdicts %.2f ms\n",
+                 m, (unsigned long long)nv, ms(t2 - t1), ms(clk::now() - t2));
   }
   return r;
 }
@@ -1486,8 +1530,6 @@ int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets
     if (offsets[c + 1] < offsets[c]) return set_err(NWC_ERR_ARG, "offsets not monotone at %zu", c);
   const uint64_t nv = offsets[m];
   if (nv && (!pks || !sigs)) return set_err(NWC_ERR_ARG, "null vote buffer");
-  std::vector<uint32_t> mi(nv);
-  for (size_t c = 0; c < m; ++c) std::fill(mi.begin() + offsets[c], mi.begin() + offsets[c + 1], (uint32_t)c);
   const int nd = (int)g_devs.size();
   std::vector<uint64_t> cuts(nd + 1);
   nwc_cert_cuts(offsets, m, (uint32_t)nd, cuts.data());
@@ -1495,7 +1537,7 @@ int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets
   std::vector<std::vector<uint64_t>> parts(nd);
   std::vector<std::thread> th;
   for (int i = 0; i < nd; ++i)
-    th.emplace_back([&, i] { rc[i] = straus_range(i, digests, m, mi.data(), pks, sigs, cuts[i], cuts[i + 1], parts[i]); });
+    th.emplace_back([&, i] { rc[i] = straus_range(i, digests, m, offsets, pks, sigs, cuts[i], cuts[i + 1], parts[i]); });
   for (auto& t : th) t.join();
   for (int r : rc) if (r < 0) return r;
   return batch_verdicts(offsets, m, cuts, parts, cert_ok_bitmap, bad_vote_bitmap);

@@ -62,6 +62,47 @@ def test_batch_many_host_chunks(oracle):
     _lib.check(lib.nwc_set_committee(None, 0))
 
 
+def test_batch_many_ragged_device_index(oracle):
+    """Certificates of 0..130 votes (empty ones first, last and inside) at the three host-call sizes:
+    packed into pinned memory, one copy (non-pipelined) and pipelined chunks.  The two larger ones
+    build the vote -> certificate index on the device (k_cert_index) from the offsets; the Straus
+    entry the same way.  Votes reuse a table of 100 keys x 40 digests, so any vote is cheap to make."""
+    from narwhal_amd import _lib
+    lib = _lib.load()
+    _lib.check(lib.nwc_set_committee(None, 0))
+    rng = np.random.default_rng(83)
+    N, D = 100, 40
+    seeds = rng.integers(0, 256, (N, 32), dtype=np.uint8)
+    dig = rng.integers(0, 256, (D, 32), dtype=np.uint8)
+    pk_t, sig_t = oracle.keygen_sign_many(np.repeat(seeds, D, axis=0), np.tile(dig, (N, 1)))   # row k * D + d
+    for target in (3000, 100_000, 300_000):
+        m = target // 65 + 1
+        counts = rng.integers(0, 131, m)
+        counts[[0, m // 2, m - 1]] = 0
+        offs = np.zeros(m + 1, np.uint32)
+        offs[1:] = np.cumsum(counts)
+        nv = int(offs[-1])
+        dc = rng.integers(0, D, m)
+        vote_cert = np.repeat(np.arange(m), counts)
+        rows = rng.integers(0, N, nv) * D + dc[vote_cert]
+        pks, sigs = pk_t[rows], sig_t[rows].copy()
+        bad = rng.random(nv) < 0.01
+        sigs[bad, 7] ^= 0x10
+        digs = np.ascontiguousarray(dig[dc])
+        exp_cert = np.bincount(vote_cert[bad], minlength=m) == 0
+        if target == 3000:
+            ocert, obad = oracle.batch_many(digs, offs, pks, sigs)
+            assert (obad == bad).all() and (ocert == exp_cert).all()
+        entries = [lib.nwc_verify_batch_many] + ([lib.nwc_verify_batch_straus_many] if target < 300_000 else [])
+        for fn in entries:
+            cert = ctypes.create_string_buffer((m + 7) // 8)
+            badb = ctypes.create_string_buffer((nv + 7) // 8)
+            _lib.check(fn(_lib.buf(digs), _lib.buf(offs), _lib.buf(pks), _lib.buf(sigs), m, cert, badb))
+            assert (_bits(badb, nv) == bad).all(), (target, fn.__name__, np.nonzero(_bits(badb, nv) != bad)[0][:10])
+            assert (_bits(cert, m) == exp_cert).all(), (target, fn.__name__, np.nonzero(_bits(cert, m) != exp_cert)[0][:10])
+    _lib.check(lib.nwc_set_committee(None, 0))
+
+
 def test_sanitize_messages_host_staged():
     """nwc_sanitize_messages on a batch above the staging threshold (4 MB of wire bytes, through the
     pinned stages): the golden wire fixtures tiled ~500 times, every code and digest as the fixture
