@@ -14,6 +14,8 @@ TAG=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
+# the library these passes profile (narwhal_amd/build.py embeds a hash of its sources)
+(cd $R && python3 -c "from narwhal_amd import build; print(build.embedded_id())") > $OUT/build_id.txt
 cd /tmp && export TMPDIR=/tmp
 ARGS="--steps 5 --warmup 1 --cpu-budget 0 --cfg1-calls 0 --cfg3-certs 0 --wire-certs 0 --cfg5-total 0 --e2e-reps 0"
 P="timeout -k 10 240 rocprofv3"

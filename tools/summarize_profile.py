@@ -25,6 +25,8 @@ def kname(full):
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "build_id.txt")):
+        shutil.copy(os.path.join(src, "build_id.txt"), os.path.join(dst, "build_id.txt"))
     c3 = os.path.join(src, "trace_cfg3", "run_kernel_stats.csv")
     if os.path.exists(c3):
         shutil.copy(c3, os.path.join(dst, "kernel_stats_cfg3.csv"))
