@@ -155,7 +155,9 @@ def buf(b) -> ctypes.c_void_p:
             # the C side reads nbytes contiguous bytes from the first element
             if not b.flags.c_contiguous:
                 raise TypeError("non-contiguous array: pass np.ascontiguousarray(a)")
-            return ctypes.c_void_p(b.ctypes.data)
+            # data_as keeps a reference to the array: a temporary (buf(x.cpu().numpy())) stays alive
+            # for as long as the returned pointer does, i.e. through the call it is passed to
+            return b.ctypes.data_as(ctypes.c_void_p)
     except ImportError:
         pass
     if isinstance(b, bytes):

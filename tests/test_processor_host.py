@@ -121,3 +121,17 @@ def test_buf_rejects_non_contiguous_arrays():
         raise AssertionError("strided view accepted")
     except TypeError:
         pass
+
+
+def test_buf_keeps_temporary_arrays_alive():
+    """buf(x.cpu().numpy()) passes a temporary: the pointer must keep the array alive through the
+    call it is an argument of (a raw address would dangle as soon as buf returned)."""
+    import ctypes
+    import gc
+    import numpy as np
+    from narwhal_amd import _lib
+    p = _lib.buf(np.arange(1 << 20, dtype=np.uint8) + 7)
+    gc.collect()
+    junk = [np.full(1 << 20, 0xEE, np.uint8) for _ in range(16)]   # would reuse freed memory
+    assert ctypes.string_at(p.value, 4) == bytes([7, 8, 9, 10])
+    del junk
