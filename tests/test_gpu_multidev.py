@@ -65,3 +65,42 @@ def test_contexts_match_oracle(oracle, tmp_path, contexts):
     raw = blob.tobytes()
     for i in range(len(lens)):
         assert got["digests"][i].tobytes() == hashlib.sha512(raw[boffs[i]:boffs[i + 1]]).digest()[:32], i
+
+
+def test_contexts_device_vote_index(tmp_path):
+    """Ragged certificates (0..130 votes, empty ones included) over 3 contexts with ~280k votes per
+    context: every shard takes the pipelined path and builds its vote -> certificate index on the
+    device (k_cert_index) from a range starting at a certificate boundary lo > 0.
+    Votes reuse a table of 100 keys x 40 digests; expected verdicts come from the construction."""
+    from tests.conftest import ROOT as root
+    from tests.oracle_lib import load_oracle
+    oracle = load_oracle()
+    rng = np.random.default_rng(37)
+    K, D = 100, 40
+    seeds = rng.integers(0, 256, (K, 32), dtype=np.uint8)
+    dtab = rng.integers(0, 256, (D, 32), dtype=np.uint8)
+    pk_t, sig_t = oracle.keygen_sign_many(np.repeat(seeds, D, axis=0), np.tile(dtab, (K, 1)))
+    m = 13000
+    counts = rng.integers(0, 131, m)
+    counts[[0, 4333, 8666, m - 1]] = 0
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint32)
+    nv = int(offs[-1])
+    dc = rng.integers(0, D, m)
+    vote_cert = np.repeat(np.arange(m), counts)
+    rows = rng.integers(0, K, nv) * D + dc[vote_cert]
+    vp, vs = pk_t[rows], sig_t[rows].copy()
+    bad = rng.random(nv) < 0.01
+    vs[bad, 9] ^= 0x20
+    dig = np.ascontiguousarray(dtab[dc])
+    np.savez(tmp_path / "in.npz", m=np.zeros((nv, 32), np.uint8), p=vp, s=vs, offs=offs, dig=dig,
+             blob=np.zeros(16, np.uint8), boffs=np.zeros(2, np.uint64))
+    env = dict(os.environ, NWC_VIRTUAL_DEVICES="3")
+    subprocess.run([sys.executable, os.path.join(root, "tests", "multidev_helper.py"), str(tmp_path / "in.npz"),
+                    str(tmp_path / "out.npz"), root], env=env, check=True, timeout=300)
+    got = np.load(tmp_path / "out.npz")
+    assert int(got["devices"][0]) == 3
+    bits = lambda raw, k: np.unpackbits(raw, bitorder="little")[:k].astype(bool)  # noqa: E731
+    exp_cert = np.bincount(vote_cert[bad], minlength=m) == 0
+    for c, b in (("cert", "bad"), ("cert_straus", "bad_straus")):
+        assert (bits(got[b], nv) == bad).all(), (b, np.nonzero(bits(got[b], nv) != bad)[0][:10])
+        assert (bits(got[c], m) == exp_cert).all(), (c, np.nonzero(bits(got[c], m) != exp_cert)[0][:10])
