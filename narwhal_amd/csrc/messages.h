@@ -456,8 +456,10 @@ __device__ uint64_t canon_entries(const uint8_t* base, uint64_t src, uint64_t cn
 
 // One wave (64-thread block) per message.  Every lane runs the sequential field decoding (same
 // instructions, no divergence); vote-, payload- and digest-input loops are split across lanes.
+// Dynamic LDS: one word per committee member (4 * min(cc.n, MSG_MAX_COMMITTEE) bytes, at least 4), so
+// a 100-node committee takes 400 B per wave and the kernel's occupancy is set by its VGPRs.
 __global__ __launch_bounds__(64) void k_parse_messages(MsgArgs a, Committee cm, CommitteeCfg cc) {
-  __shared__ u32 first[MSG_MAX_COMMITTEE];   // first vote position of each committee member
+  extern __shared__ u32 first[];   // first vote position of each committee member
   const uint64_t i = blockIdx.x;
   const u32 lane = threadIdx.x;
   if (i >= a.m) return;   // block-uniform
@@ -578,7 +580,7 @@ __global__ __launch_bounds__(64) void k_parse_messages(MsgArgs a, Committee cm, 
           a.v_msg[vbase + v] = (uint32_t)i;
           const int kidx = committee_lookup(cm, key);
           weight += member_stake(cc, kidx);
-          if (kidx >= 0 && kidx < (int)MSG_MAX_COMMITTEE) atomicMin(&first[kidx], (u32)(v < 0xFFFFFFF0u ? v : 0xFFFFFFF0u));
+          if (kidx >= 0 && kidx < (int)ncm) atomicMin(&first[kidx], (u32)(v < 0xFFFFFFF0u ? v : 0xFFFFFFF0u));
         }
         const u32 fmin = wave_min_u32(fpos);
         if (fmin != 0xFFFFFFFFu) {
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(64) void k_parse_messages(MsgArgs a, Committee cm, 
             u32 key[8];
             _Pragma("unroll") for (int k = 0; k < 8; ++k) key[k] = kw[k];
             const int kidx = committee_lookup(cm, key);
-            const bool reused = kidx >= 0 && kidx < (int)MSG_MAX_COMMITTEE && first[kidx] < (u32)v;
+            const bool reused = kidx >= 0 && kidx < (int)ncm && first[kidx] < (u32)v;
             const bool unknown = member_stake(cc, kidx) == 0;
             if ((reused || unknown) && (u32)v < err) { err = (u32)v; err_kind = reused ? DAG_AUTHORITY_REUSE : DAG_UNKNOWN_AUTHORITY; }
           }

@@ -109,6 +109,7 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;      // small batch-leaf calls: the keys' torsion test beside the verification
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_msg = nullptr;   // sanitize: k_header_digests done on the side stream
   // large host calls: input chunks are copied on `xfer` while the previous chunk verifies on
   // `stream` (one event per chunk in flight, created on first use)
   hipStream_t xfer = nullptr;
@@ -295,6 +296,7 @@ int init_device(DevCtx& d) {
   HIP_TRY(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&d.ev_msg, hipEventDisableTiming));
   d.cus = prop.multiProcessorCount;
   int bpc = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify<true, false>), 256, 0));
@@ -1428,6 +1430,7 @@ void nwc_shutdown(void) {
     if (d->side) (void)hipStreamSynchronize(d->side);
     if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
     if (d->ev_join) (void)hipEventDestroy(d->ev_join);
+    if (d->ev_msg) (void)hipEventDestroy(d->ev_msg);
     if (d->side) (void)hipStreamDestroy(d->side);
     if (d->xfer) (void)hipStreamSynchronize(d->xfer);
     if (d->stager) d->stager->release();
@@ -1912,10 +1915,16 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   HIP_TRY(hipMemsetAsync(a.v_msg, 0, 4 * vcap, s));
   const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
   const nwc::CommitteeCfg cc{d.cc_stakes, d.cc_worker_off, d.cc_worker_ids, d.cc_quorum, d.cc_n};
-  hipLaunchKernelGGL(nwc::k_parse_messages, dim3((unsigned)m), dim3(64), 0, s, a, cm, cc);
+  const size_t first_lds = 4 * (size_t)std::max<uint32_t>(1, std::min<uint32_t>(d.cc_n, nwc::MSG_MAX_COMMITTEE));
+  hipLaunchKernelGGL(nwc::k_parse_messages, dim3((unsigned)m), dim3(64), first_lds, s, a, cm, cc);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(nwc::k_header_digests, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a);
+  // Header::digest checks on the side stream, beside the signature launches (only the final
+  // kernel reads their result); launch_verify's own side-stream work queues behind them
+  HIP_TRY(hipEventRecord(d.ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(d.side, d.ev_fork, 0));
+  hipLaunchKernelGGL(nwc::k_header_digests, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.side, a);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(d.ev_msg, d.side));
   uint32_t nv = 0;
   HIP_TRY(hipMemcpyAsync(&nv, a.v_total, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -1924,6 +1933,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, m, 1, sbits, s)) return rc;
   if (nvotes)
     if (int rc = launch_verify(d, a.cdig, a.v_msg, 0, a.v_pk, a.v_sig, nvotes, 0, lbits, s)) return rc;
+  HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
   hipLaunchKernelGGL(nwc::k_finalize_messages, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a.rec,
                      a.rec_n, a.hmatch, sbits, lbits, (uint64_t)m, dcodes);
   HIP_TRY(hipGetLastError());
