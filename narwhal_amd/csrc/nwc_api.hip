@@ -110,6 +110,7 @@ struct DevCtx {
   hipStream_t side = nullptr;      // small batch-leaf calls: the keys' torsion test beside the verification
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_msg = nullptr;   // sanitize: k_header_digests done on the side stream
+  hipEvent_t ev_count = nullptr; // sanitize: the vote count has reached the host
   // large host calls: input chunks are copied on `xfer` while the previous chunk verifies on
   // `stream` (one event per chunk in flight, created on first use)
   hipStream_t xfer = nullptr;
@@ -297,6 +298,7 @@ int init_device(DevCtx& d) {
   HIP_TRY(hipEventCreateWithFlags(&d.ev_fork, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&d.ev_msg, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&d.ev_count, hipEventDisableTiming));
   d.cus = prop.multiProcessorCount;
   int bpc = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify<true, false>), 256, 0));
@@ -1431,6 +1433,7 @@ void nwc_shutdown(void) {
     if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
     if (d->ev_join) (void)hipEventDestroy(d->ev_join);
     if (d->ev_msg) (void)hipEventDestroy(d->ev_msg);
+    if (d->ev_count) (void)hipEventDestroy(d->ev_count);
     if (d->side) (void)hipStreamDestroy(d->side);
     if (d->xfer) (void)hipStreamSynchronize(d->xfer);
     if (d->stager) d->stager->release();
@@ -1925,12 +1928,17 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   hipLaunchKernelGGL(nwc::k_header_digests, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.side, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(d.ev_msg, d.side));
-  uint32_t nv = 0;
-  HIP_TRY(hipMemcpyAsync(&nv, a.v_total, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  const uint64_t nvotes = std::min<uint64_t>(nv, vcap);
-  // the signature equations: strict (headers' and votes' signatures), batch leaves (votes)
+  // the vote count sizes the leaf launch: read it behind the parse, and let the strict launch
+  // (headers' and votes' signatures, which does not need it) run while the host waits for it
+  // (into pinned memory: a pageable destination would make the copy synchronous)
+  if (int rc = d.ensure_pinned(NWC_PINNED_STAGE_MAX)) return rc;
+  uint32_t* nv_host = reinterpret_cast<uint32_t*>(d.pinned);
+  HIP_TRY(hipMemcpyAsync(nv_host, a.v_total, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(d.ev_count, s));
   if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, m, 1, sbits, s)) return rc;
+  HIP_TRY(hipEventSynchronize(d.ev_count));
+  const uint64_t nvotes = std::min<uint64_t>(*nv_host, vcap);
+  // the batch leaves (certificate votes)
   if (nvotes)
     if (int rc = launch_verify(d, a.cdig, a.v_msg, 0, a.v_pk, a.v_sig, nvotes, 0, lbits, s)) return rc;
   HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
