@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -227,6 +228,9 @@ struct DevCtx {
 #endif
 #ifndef NWC_HOST_CHUNK_MAX
 #define NWC_HOST_CHUNK_MAX (1u << 20)
+#endif
+#ifndef NWC_MSG_CHUNK
+#define NWC_MSG_CHUNK (72u << 20)   // bytes of wire messages per pipelined chunk of nwc_sanitize_messages (A/B: profiles/r04/ab_wire_host_chunks.txt)
 #endif
 #ifndef NWC_HOST_CHUNK_GROWTH
 #define NWC_HOST_CHUNK_GROWTH 3
@@ -1985,23 +1989,86 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
   uint8_t* ddig = digests32 ? c.take<uint8_t>(32 * m) : nullptr;
   std::vector<uint64_t> hoff(m + 1);
   for (size_t i = 0; i <= m; ++i) hoff[i] = offsets[i] - base;
-  if (host_staging() && total >= ((size_t)4 << 20)) {
-    // large batches (config 3 from the wire: 10 KB per certificate) through the pinned stages on
-    // the transfer stream, after every launch that may still read the arena
+  const bool staged = host_staging() && total >= ((size_t)4 << 20);
+  // Large batches (config 3 from the wire: 10 KB per certificate) go through the pinned stages on
+  // the transfer stream in chunks of ~NWC_MSG_CHUNK bytes cut on message boundaries; chunk k is
+  // parsed and verified while chunk k + 1 crosses PCIe.  The chunks share the message offsets
+  // (uploaded first, relative to ddata) and the message arena (sanitize_dev, run per chunk in
+  // stream order).
+  static const uint64_t msg_chunk = [] {
+    const char* e = std::getenv("NWC_MSG_CHUNK");   // 0 = one copy, then one pass (A/B)
+    return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)NWC_MSG_CHUNK;
+  }();
+  std::vector<size_t> cuts{0};
+  if (staged && msg_chunk && total >= 2 * msg_chunk) {
+    const uint64_t nch = (total + msg_chunk - 1) / msg_chunk;
+    for (uint64_t k = 1; k < nch; ++k) {
+      const size_t cm = (size_t)(std::lower_bound(hoff.begin(), hoff.end(), total * k / nch) - hoff.begin());
+      if (cm > cuts.back() && cm < m) cuts.push_back(cm);
+    }
+  }
+  cuts.push_back(m);
+  const size_t nch = cuts.size() - 1;
+  HIP_TRY(hipMemsetAsync(ddata + total, 0, 16, d.stream));
+  HIP_TRY(hipMemcpyAsync(doff, hoff.data(), 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
+  if (!staged) {
+    HIP_TRY(hipMemcpyAsync(ddata, data + base, total, hipMemcpyHostToDevice, d.stream));
+    if (int rc = sanitize_dev(d, ddata, doff, m, total, gc_round, vote_target, dcodes, ddig, drec, d.stream)) return rc;
+  } else {
     if (int rc = ensure_stager(d)) return rc;
+    while (d.ev_chunk.size() < nch) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      d.ev_chunk.push_back(e);
+    }
+    // the copies wait for every launch that may still read the arena
     HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
     HIP_TRY(hipStreamWaitEvent(d.xfer, d.ev_fork, 0));
     d.stager->reset();
-    HIP_TRY(d.stager->put(ddata, data + base, total));
-    HIP_TRY(d.stager->flush());
-    HIP_TRY(hipEventRecord(d.ev_fork, d.xfer));
-    HIP_TRY(hipStreamWaitEvent(d.stream, d.ev_fork, 0));
-  } else {
-    HIP_TRY(hipMemcpyAsync(ddata, data + base, total, hipMemcpyHostToDevice, d.stream));
+    // a copy thread fills the stages chunk by chunk and records each chunk's event; this thread
+    // runs chunk k once its event has been recorded (a wait on an unrecorded event would not wait)
+    std::mutex cmu;
+    std::condition_variable ccv;
+    size_t recorded = 0;
+    hipError_t copy_err = hipSuccess;
+    std::thread copier([&] {
+      hipError_t e = hipSetDevice(d.hip_id);
+      for (size_t k = 0; k < nch && e == hipSuccess; ++k) {
+        const uint64_t b0 = hoff[cuts[k]], b1 = hoff[cuts[k + 1]];
+        e = d.stager->put(ddata + b0, data + base + b0, b1 - b0);
+        if (e == hipSuccess) e = d.stager->flush();
+        if (e == hipSuccess) e = hipEventRecord(d.ev_chunk[k], d.xfer);
+        std::lock_guard<std::mutex> g(cmu);
+        if (e == hipSuccess) recorded = k + 1;
+        else copy_err = e;
+        ccv.notify_all();
+      }
+    });
+    int rc = 0;
+    for (size_t k = 0; k < nch && rc == 0; ++k) {
+      {
+        std::unique_lock<std::mutex> g(cmu);
+        ccv.wait(g, [&] { return recorded > k || copy_err != hipSuccess; });
+        if (recorded <= k) {
+          rc = set_err(NWC_ERR_DEVICE, "message copy: %s", hipGetErrorString(copy_err));
+          break;
+        }
+      }
+      const hipError_t e = hipStreamWaitEvent(d.stream, d.ev_chunk[k], 0);
+      if (e != hipSuccess) {
+        rc = set_err(NWC_ERR_DEVICE, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+        break;
+      }
+      const size_t c0 = cuts[k], c1 = cuts[k + 1];
+      rc = sanitize_dev(d, ddata, doff + c0, c1 - c0, total, gc_round, vote_target, dcodes + c0,
+                        ddig ? ddig + 32 * c0 : nullptr, drec + 4 * c0, d.stream);
+    }
+    copier.join();
+    if (rc) {
+      (void)hipStreamSynchronize(d.xfer);   // no copy still writes the arena when the call returns
+      return rc;
+    }
   }
-  HIP_TRY(hipMemsetAsync(ddata + total, 0, 16, d.stream));
-  HIP_TRY(hipMemcpyAsync(doff, hoff.data(), 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
-  if (int rc = sanitize_dev(d, ddata, doff, m, total, gc_round, vote_target, dcodes, ddig, drec, d.stream)) return rc;
   HIP_TRY(hipMemcpyAsync(codes, dcodes, 4 * m, hipMemcpyDeviceToHost, d.stream));
   std::vector<uint32_t> rec;
   if (kinds) {

@@ -107,6 +107,27 @@ def test_sanitize_messages_host_staged():
     """nwc_sanitize_messages on a batch above the staging threshold (4 MB of wire bytes, through the
     pinned stages): the golden wire fixtures tiled ~500 times, every code and digest as the fixture
     says (primary/src/core.rs:306-346 via the restatement, tests/golden/messages.json)."""
+    _sanitize_tiled_golden()
+
+
+def test_sanitize_messages_host_chunks():
+    """The same batch in 1-MB pipelined chunks (NWC_MSG_CHUNK, read once per process: a child
+    process): ~8 chunks cut on message boundaries, each parsed and verified while the next one
+    crosses PCIe, codes and digests unchanged."""
+    import os
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from tests.test_gpu_host_paths import _sanitize_tiled_golden\n"
+            "_sanitize_tiled_golden()\n"
+            "print('done', flush=True)\n" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=ROOT,
+                       env=dict(os.environ, NWC_MSG_CHUNK=str(1 << 20)))
+    assert r.returncode == 0 and "done" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-3000:])
+
+
+def _sanitize_tiled_golden():
     import json
     import os
     from narwhal_amd import _lib
