@@ -75,6 +75,29 @@ def test_c_host_golden(golden_verify, golden_batch, golden_sha):
     assert not bad, bad[:5]
 
 
+def _report_head(err):
+    """The sanitizer report's first lines (error kind, access, the faulting stack), not its tail."""
+    i = err.find("==ERROR")
+    if i < 0:
+        i = err.find("runtime error")
+    return err[max(0, i - 200):i + 4000] if i >= 0 else err[-3000:]
+
+
+def _keep_report(name, r):
+    """A failing sanitizer run's whole stdout/stderr, kept where a GPU-box run's outputs come back."""
+    import os
+    from tests.conftest import ROOT
+    d = os.path.join(ROOT, "gpurun_out")
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".stderr"), "w") as f:
+            f.write(r.stderr)
+        with open(os.path.join(d, name + ".stdout"), "w") as f:
+            f.write(r.stdout)
+    except OSError:
+        pass
+
+
 def test_c_host_under_asan(oracle, golden_verify, golden_batch):
     """libnwc's host code (small-call staging, zero-copy path, auto key cache, shard threads and
     bitmap merges over NWC_VIRTUAL_DEVICES=3 contexts, certificate cuts, concurrent callers)
@@ -148,7 +171,9 @@ def test_c_host_under_asan(oracle, golden_verify, golden_batch):
     env = dict(os.environ, NWC_VIRTUAL_DEVICES="3", ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([ASAN_BIN], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=600, env=env)
-    assert r.returncode == 0, (r.returncode, r.stdout[-500:], r.stderr[-3000:])
+    if r.returncode != 0:
+        _keep_report("abi_host_asan", r)
+    assert r.returncode == 0, (r.returncode, r.stdout[-500:], _report_head(r.stderr))
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
     got = [l.rstrip() for l in r.stdout.splitlines()]
     assert len(got) == len(want), (len(got), len(want), r.stderr[-1000:])
