@@ -93,6 +93,10 @@ def main():
                     help="K > 0: signers drawn from K keys that are NOT registered (launch keys)")
     ap.add_argument("--call", type=int, default=0, help="C > 0: device calls of at most C equations")
     ap.add_argument("--straus", action="store_true", help="also the Straus sub-batch path (per-vote bits vs the oracle)")
+    ap.add_argument("--host-batch", action="store_true",
+                    help="also nwc_verify_batch_many from host memory: each chunk's triples in ragged certificates "
+                         "(0..130 votes, votes signing their certificate's digest before mutation), certificate and "
+                         "bad-vote bits vs the oracle's batch_many on the same inputs")
     ap.add_argument("--valid-frac", type=float, default=0.30,
                     help="share of unmutated triples (0.99: most Straus sub-batches pass, the rest exercise the leaves)")
     args = ap.parse_args()
@@ -114,6 +118,7 @@ def main():
     rng = np.random.default_rng(20261016)
     stats = {c: {"n": 0, "strict_valid": 0, "leaf_valid": 0, "strict_mismatch": 0, "leaf_mismatch": 0,
                  "straus_mismatch": 0, "randomized": 0, "straus_randomized_pass": 0} for c in CLASSES}
+    host_batch = {"votes": 0, "certificates": 0, "bad_votes": 0, "failing_certificates": 0, "mismatch": 0}
     t0 = time.time()
     done = 0
     mism = []
@@ -127,7 +132,19 @@ def main():
             seeds = lseeds[who]
         else:
             seeds = device.derive32(b"soak-seed", done, n)
-        msgs = device.derive32(b"soak-msg", done, n)
+        if args.host_batch:
+            # ragged certificates over this chunk's triples; vote v signs its certificate's digest
+            counts = []
+            while sum(counts) < n:
+                counts.append(int(rng.integers(0, 131)))
+            counts[-1] -= sum(counts) - n
+            offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint32)
+            ncert = len(counts)
+            cdig = device.derive32(b"soak-cert", done, ncert).cpu().numpy().copy()
+            vote_cert = np.repeat(np.arange(ncert), counts)
+            msgs = torch.from_numpy(np.ascontiguousarray(cdig[vote_cert])).cuda()
+        else:
+            msgs = device.derive32(b"soak-msg", done, n)
         pks, sigs = device.keygen_sign(seeds, msgs)
         torch.cuda.synchronize()
         m, p, s = (t.cpu().numpy().copy() for t in (msgs, pks, sigs))
@@ -150,6 +167,22 @@ def main():
         else:
             gb = np.zeros(n, bool)
             rnd = smis = np.zeros(n, bool)
+        hb_mis = 0
+        if args.host_batch:
+            import ctypes
+            cert = ctypes.create_string_buffer((ncert + 7) // 8)
+            badb = ctypes.create_string_buffer((n + 7) // 8)
+            _lib.check(lib.nwc_verify_batch_many(_lib.buf(cdig), _lib.buf(offs), _lib.buf(p), _lib.buf(s), ncert,
+                                                 cert, badb))
+            ocert, obad = orc.batch_many(cdig, offs, p, s, threads=threads)
+            hbad = np.unpackbits(np.frombuffer(badb.raw, np.uint8), bitorder="little")[:n].astype(bool)
+            hcert = np.unpackbits(np.frombuffer(cert.raw, np.uint8), bitorder="little")[:ncert].astype(bool)
+            hb_mis = int((hbad != obad.astype(bool)).sum()) + int((hcert != ocert.astype(bool)).sum())
+            host_batch["votes"] += n
+            host_batch["certificates"] += ncert
+            host_batch["bad_votes"] += int(obad.sum())
+            host_batch["failing_certificates"] += int((~ocert.astype(bool)).sum())
+            host_batch["mismatch"] += hb_mis
         for j in np.nonzero((gs != os_) | (gl != ol) | smis)[0][:20]:
             mism.append({"class": CLASSES[kind[j]], "index": int(done + j), "msg": m[j].tobytes().hex(),
                          "pk": p[j].tobytes().hex(), "sig": s[j].tobytes().hex(), "gpu_strict": bool(gs[j]),
@@ -177,13 +210,14 @@ def main():
         _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
         held = h.value
     out = {"triples": args.n, "committee": args.committee, "launch_keys": args.launch_keys, "launch_keys_held": held,
-           "call": args.call, "straus": args.straus,
+           "call": args.call, "straus": args.straus, "host_batch": host_batch if args.host_batch else None,
            "valid_frac": args.valid_frac, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
            "mismatches": mism}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(out, open(args.out, "w"), indent=1)
-    print(json.dumps(total))
-    return 0 if total["strict_mismatch"] == 0 and total["leaf_mismatch"] == 0 and total["straus_mismatch"] == 0 else 1
+    print(json.dumps(dict(total, host_batch_mismatch=host_batch["mismatch"])))
+    return 0 if (total["strict_mismatch"] == 0 and total["leaf_mismatch"] == 0 and total["straus_mismatch"] == 0
+                 and host_batch["mismatch"] == 0) else 1
 
 
 if __name__ == "__main__":
