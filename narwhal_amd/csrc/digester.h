@@ -14,6 +14,10 @@
 // larger than NWC_DIGEST_KEEP_BYTES (1 GiB) is released after its group, so one 100k-batch group
 // does not keep 50 GB resident (nwc_memory_info reports what a digester holds).
 //
+// Receive arena (nwc_digester_arena): batches the caller placed in the digester's pinned arena are
+// DMA'd into the arena's device mirror while their group is still being collected (runs of >= 8 MB),
+// and the kernel reads them there; the stage path below is skipped for such a group.
+//
 // Data path per group: the borrowed batches are gathered into NWC_DIGEST_STAGES (4) pinned 32-MB
 // stages in rotation (16-byte-aligned starts, the kernel's dwordx4 path; each stage filled by a
 // fixed pool of up to 8 host threads) and DMA'd on the digester's own stream into one device
@@ -68,8 +72,12 @@ struct Digester {
   // whose batches all lie in it, packed at 16-byte-rounded strides, is DMA'd without a stage fill
   uint8_t* arena = nullptr;
   size_t arena_size = 0;
+  // its device mirror: arena bytes [o, o + len) of a submitted batch are DMA'd to darena + o while
+  // the drain thread is still collecting the group, so a group of arena batches launches as soon
+  // as it closes (drain thread only; allocated at the first such group, arena_size bytes)
+  uint8_t* darena = nullptr;
+  std::atomic<size_t> darena_cap{0};
   std::atomic<uint64_t> direct_groups{0};
-  static constexpr size_t MAX_DIRECT_RUNS = 1024;
 
   int init() {
     pool.start(copy_threads);
@@ -97,11 +105,53 @@ struct Digester {
     if (hse) (void)hipHostFree(hse);
     if (hout) (void)hipHostFree(hout);
     if (arena) (void)hipHostFree(arena);
+    if (darena) (void)hipFree(darena);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
   // device bytes the batch takes in a group's buffer (16-byte aligned starts)
   static uint64_t padded(size_t len) { return (len + 15) & ~(uint64_t)15; }
+
+  // the group being collected: all of its batches in the arena so far, and how many of them have
+  // had their DMA queued (drain thread only)
+  bool mirrored = false;
+  size_t mirrored_sent = 0;
+  uint64_t mirror_pending = 0;   // bytes of g[mirrored_sent..]
+  // collected arena bytes are DMA'd in runs of at least this much (many small DMAs of single
+  // 500-KB batches ran at half the copy engine's rate); the rest when the group closes
+  static constexpr uint64_t MIRROR_CHUNK = 8u << 20;
+  uint64_t mirror_runs = 0;    // DMAs queued for the current group (NWC_DIGEST_TIMING)
+  int pending_err = 0;
+  bool in_arena(const Item& it) const {
+    return it.len == 0 || (arena && it.p >= arena && (size_t)(it.p - arena) <= arena_size &&
+                           it.len <= arena_size - (size_t)(it.p - arena));
+  }
+  // Queues the DMAs of g[sent..] (arena batches) into the arena's device mirror at their arena
+  // offsets: one DMA per run of batches adjacent in the arena (gaps under 256 bytes are copied
+  // along).  Drain thread only.
+  int stream_arena(const std::vector<Item>& g, size_t& sent) {
+    if (!darena) {
+      HIP_TRY(hipMalloc(&darena, arena_size));
+      darena_cap = arena_size;
+    }
+    size_t i = sent;
+    while (i < g.size()) {
+      if (g[i].len == 0) { ++i; continue; }
+      const size_t o = (size_t)(g[i].p - arena);
+      size_t e = o + g[i].len, j = i + 1;
+      for (; j < g.size(); ++j) {
+        if (g[j].len == 0) continue;
+        const size_t oj = (size_t)(g[j].p - arena);
+        if (oj < e || oj > e + 256) break;
+        e = oj + g[j].len;
+      }
+      HIP_TRY(hipMemcpyAsync(darena + o, arena + o, e - o, hipMemcpyHostToDevice, stream));
+      ++mirror_runs;
+      i = j;
+    }
+    sent = g.size();
+    return 0;
+  }
 
   // SHA-512[..32] of every batch of the group into out32 (32 bytes each)
   int digest_group(const std::vector<Item>& g, uint8_t* out32) {
@@ -120,48 +170,40 @@ struct Digester {
       HIP_TRY(hipHostMalloc(&hout, 32 * nk, hipHostMallocDefault));
       k_cap = nk;
     }
-    uint64_t total = 0;
-    for (size_t i = 0; i < k; ++i) {
-      hse[i] = total;
-      hse[k + i] = total + g[i].len;
-      total += padded(g[i].len);
-    }
-    if (total + 16 > ddata_cap) {
-      if (ddata) HIP_TRY(hipFree(ddata));
-      ddata = nullptr;
-      ddata_cap = 0;
-      // headroom for slightly larger groups, but never past the per-launch cap
-      const size_t cap = std::max<size_t>(total + 16, std::min<size_t>((total + 16) + (total + 16) / 4, max_bytes + 16));
-      HIP_TRY(hipMalloc(&ddata, cap));
-      ddata_cap = cap;
+    if (int rc = pending_err) {   // a DMA of the arena mirror failed while the group was collected
+      pending_err = 0;
+      return rc;
     }
     using clk = std::chrono::steady_clock;
     double t_wait = 0, t_fill = 0;
     const auto t_start = clk::now();
-    // direct path: every batch in the receive arena, consecutive batches at the device layout's
-    // spacing (runs of them are one DMA each, straight from the arena into HBM)
-    std::vector<std::pair<size_t, size_t>> runs;   // [first, last] non-empty batches of each run
-    bool direct = arena != nullptr;
-    for (size_t i = 0; direct && i < k; ++i) {
-      if (g[i].len == 0) continue;   // nothing to move; never breaks a run
-      const uint8_t* p = g[i].p;
-      if (!(p >= arena && (size_t)(p - arena) <= arena_size && g[i].len <= arena_size - (size_t)(p - arena))) {
-        direct = false;
-        break;
-      }
-      // a run continues while batch i sits where the device layout puts it relative to the run's first
-      if (!runs.empty() && (uint64_t)(p - g[runs.back().first].p) == hse[i] - hse[runs.back().first])
-        runs.back().second = i;
-      else if (runs.size() < MAX_DIRECT_RUNS)
-        runs.emplace_back(i, i);
-      else
-        direct = false;
-    }
+    // mirror path: every batch in the receive arena, most of its bytes already on their way into
+    // the arena's device mirror (stream_arena, queued while the group was collected): the kernel
+    // reads them in place there.  Otherwise the batches are gathered into the group's buffer.
+    const bool direct = mirrored;
+    uint64_t total = 0;
     if (direct) {
-      for (const auto& r : runs)   // the run's bytes, source and device at the same relative offsets
-        HIP_TRY(hipMemcpyAsync(ddata + hse[r.first], g[r.first].p, hse[k + r.second] - hse[r.first],
-                               hipMemcpyHostToDevice, stream));
+      if (int rc = stream_arena(g, mirrored_sent)) return rc;
+      for (size_t i = 0; i < k; ++i) {
+        hse[i] = g[i].len ? (uint64_t)(g[i].p - arena) : 0;
+        hse[k + i] = hse[i] + g[i].len;
+      }
       ++direct_groups;
+    } else {
+      for (size_t i = 0; i < k; ++i) {
+        hse[i] = total;
+        hse[k + i] = total + g[i].len;
+        total += padded(g[i].len);
+      }
+      if (total + 16 > ddata_cap) {
+        if (ddata) HIP_TRY(hipFree(ddata));
+        ddata = nullptr;
+        ddata_cap = 0;
+        // headroom for slightly larger groups, but never past the per-launch cap
+        const size_t cap = std::max<size_t>(total + 16, std::min<size_t>((total + 16) + (total + 16) / 4, max_bytes + 16));
+        HIP_TRY(hipMalloc(&ddata, cap));
+        ddata_cap = cap;
+      }
     }
     // gather through the pinned stages: fill one (with copy_threads host threads, each a
     // contiguous byte range of the stage) while the others' DMA is in flight.  Stage s covers the
@@ -199,7 +241,7 @@ struct Digester {
       s = (s + 1) % nstages;
     }
     HIP_TRY(hipMemcpyAsync(dse, hse, 16 * k, hipMemcpyHostToDevice, stream));
-    if (int rc = launch_digest(ddata, dse, dse + k, k, dout, stream)) return rc;
+    if (int rc = launch_digest(direct ? darena : ddata, dse, dse + k, k, dout, stream)) return rc;
     HIP_TRY(hipMemcpyAsync(hout, dout, 32 * k, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     std::memcpy(out32, hout, 32 * k);
@@ -209,8 +251,8 @@ struct Digester {
       ddata_cap = 0;
     }
     if (timing && direct)
-      std::fprintf(stderr, "nwc digester: group %zu, %.1f MB (arena, %zu direct DMA runs): gathered in %.2f ms, total %.2f ms\n", k,
-                   total / 1e6, runs.size(), std::chrono::duration<double>(t_start - t_group).count() * 1e3,
+      std::fprintf(stderr, "nwc digester: group %zu (arena mirror, %llu DMA runs): gathered in %.2f ms, total %.2f ms\n", k,
+                   (unsigned long long)mirror_runs, std::chrono::duration<double>(t_start - t_group).count() * 1e3,
                    std::chrono::duration<double>(clk::now() - t_start).count() * 1e3);
     else if (timing)
       std::fprintf(stderr, "nwc digester: group %zu, %.1f MB: gathered in %.2f ms, fill %.2f ms (%.1f GB/s), waits on DMA %.2f ms, total %.2f ms\n",
@@ -232,6 +274,10 @@ struct Digester {
         if (in.empty()) return;   // stop, drained
         g.push_back(in.front());
         in.pop_front();
+        mirrored = arena != nullptr && in_arena(g.back());
+        mirrored_sent = 0;
+        mirror_pending = g.back().len;
+        mirror_runs = 0;
         uint64_t gbytes = padded(g.back().len);
         t_group = std::chrono::steady_clock::now();
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
@@ -246,6 +292,14 @@ struct Digester {
           gbytes += padded(in.front().len);
           g.push_back(in.front());
           in.pop_front();
+          if (mirrored && !in_arena(g.back())) mirrored = false;   // a batch outside: gather the group
+          if (mirrored && (mirror_pending += g.back().len) >= MIRROR_CHUNK && !pending_err) {
+            // queue the DMAs of the arena batches collected so far; the group stays open
+            lk.unlock();
+            pending_err = stream_arena(g, mirrored_sent);
+            lk.lock();
+            mirror_pending = 0;
+          }
         }
       }
       dig.resize(32 * g.size());
@@ -282,7 +336,7 @@ uint64_t digester_device_bytes(int hip_id) {
   std::lock_guard<std::mutex> lk(g_dg_mu);
   uint64_t b = 0;
   for (const Digester* q : g_digesters)
-    if (q->hip_id == hip_id) b += q->ddata_cap.load() + 48 * (uint64_t)q->k_cap.load();
+    if (q->hip_id == hip_id) b += q->ddata_cap.load() + q->darena_cap.load() + 48 * (uint64_t)q->k_cap.load();
   return b;
 }
 

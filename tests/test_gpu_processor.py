@@ -126,10 +126,11 @@ def test_digester_stage_rotation(stages, threads):
 
 
 def test_digester_receive_arena():
-    """nwc_digester_arena: batches written into the pinned arena at 16-byte-rounded strides are
-    DMA'd straight into HBM (runs: a gap breaks a run, not the direct path); a group holding one
-    batch from outside the arena, or mis-spaced ones beyond the run limit, takes the stage path.
-    Digests equal hashlib either way, in submission order."""
+    """nwc_digester_arena: batches written into the pinned arena are DMA'd into the arena's device
+    mirror at their arena offsets while the group is collected (runs of adjacent batches; a gap,
+    odd spacing or submission out of arena order only starts a new run), and the kernel reads them
+    there; a group holding one batch from outside the arena takes the stage path.  Digests equal
+    hashlib either way, in submission order."""
     from narwhal_amd.processor import Digester
     rng = np.random.default_rng(9)
     lens = [0, 1, 15, 16, 17, 127, 128, 129, 4096, 0, 333] + [int(x) for x in rng.integers(0, 400_000, 40)]
