@@ -21,7 +21,8 @@
 // Data path per group: the borrowed batches are gathered into NWC_DIGEST_STAGES (4) pinned 32-MB
 // stages in rotation (16-byte-aligned starts, the kernel's dwordx4 path; each stage filled by a
 // fixed pool of up to 8 host threads) and DMA'd on the digester's own stream into one device
-// buffer while the next stages are filled; then k_sha512_digest32[_sched] over the group
+// buffer while the next stages are filled -- a stage as soon as all of its batches have arrived,
+// while the group is still being collected; then k_sha512_digest32[_sched] over the group
 // and one D2H of 32 bytes per batch.  The digester has its own stream and buffers (it does not
 // serialise with verification calls on the device's context).  Included by nwc_api.hip.
 #pragma once
@@ -153,6 +154,86 @@ struct Digester {
     return 0;
   }
 
+  // Stage gathering of a group that is not in the arena, also started while the group is still
+  // being collected: the device layout's offsets of the batches collected so far (16-byte aligned,
+  // in arrival order), the bytes [0, gpos) already gathered into stages and queued for DMA, and the
+  // stage rotation.  Drain thread only; reset at each group's first batch.
+  std::vector<uint64_t> gstart;
+  uint64_t gtotal = 0, gpos = 0;
+  size_t gfirst = 0;   // first batch that may overlap [gpos, ...)
+  int gstage = 0;
+  bool gused[MAX_STAGES] = {};
+  double t_wait = 0, t_fill = 0;
+  void group_reset() {
+    gstart.clear();
+    gtotal = gpos = 0;
+    gfirst = 0;
+    gstage = 0;
+    for (bool& u : gused) u = false;   // the previous group's DMAs have landed (stream synchronised)
+    t_wait = t_fill = 0;
+  }
+  void group_note(const Item& it) {
+    gstart.push_back(gtotal);
+    gtotal += padded(it.len);
+  }
+  // The group's device buffer holds [0, need) (+16 bytes of slack): a larger one keeps the bytes
+  // gathered so far, [0, gpos).  While the group grows (stages gathered during its collection) the
+  // buffer at least doubles; for a group's final size it gets a quarter of headroom, never past the
+  // per-launch cap.
+  int ensure_ddata(uint64_t need, bool growing) {
+    if (need + 16 <= ddata_cap) return 0;
+    const size_t grown = growing ? std::max<size_t>(2 * ddata_cap.load(), (size_t)64 << 20) : (need + 16) + (need + 16) / 4;
+    const size_t cap = std::max<size_t>(need + 16, std::min<size_t>(grown, max_bytes + 16));
+    uint8_t* nd = nullptr;
+    HIP_TRY(hipMalloc(&nd, cap));
+    if (ddata) {
+      if (gpos) HIP_TRY(hipMemcpyAsync(nd, ddata, gpos, hipMemcpyDeviceToDevice, stream));
+      HIP_TRY(hipStreamSynchronize(stream));   // the old buffer's DMAs and this copy are done
+      HIP_TRY(hipFree(ddata));
+    }
+    ddata = nd;
+    ddata_cap = cap;
+    return 0;
+  }
+  // Gathers the device layout's bytes [gpos, end) (at most one stage) of g's batches into the next
+  // pinned stage with copy_threads host threads (each a contiguous byte range of the stage) and
+  // queues its DMA; the other stages' DMAs stay in flight.
+  int gather_stage(const std::vector<Item>& g, uint64_t end) {
+    using clk = std::chrono::steady_clock;
+    if (int rc = ensure_ddata(end, end < gtotal)) return rc;
+    const size_t k = g.size();
+    const auto t0 = clk::now();
+    if (gused[gstage]) HIP_TRY(hipEventSynchronize(stage_ev[gstage]));   // its previous DMA has landed
+    const auto t1 = clk::now();
+    t_wait += std::chrono::duration<double>(t1 - t0).count();
+    const uint64_t pos = gpos;
+    uint8_t* const st = stage[gstage];
+    while (gfirst < k && gstart[gfirst] + g[gfirst].len <= pos) ++gfirst;   // batches wholly before pos
+    auto copy_range = [&](uint64_t lo, uint64_t hi) {
+      // batches overlapping [lo, hi), found from gfirst (starts are ascending)
+      size_t i = gfirst;
+      while (i < k && gstart[i] + g[i].len <= lo) ++i;
+      for (; i < k && gstart[i] < hi; ++i) {
+        const uint64_t a0 = std::max<uint64_t>(gstart[i], lo), a1 = std::min<uint64_t>(gstart[i] + g[i].len, hi);
+        if (a1 > a0) std::memcpy(st + (a0 - pos), g[i].p + (a0 - gstart[i]), a1 - a0);
+      }
+    };
+    const uint64_t bytes = end - pos;
+    const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(copy_threads, (bytes + (2u << 20) - 1) / (2u << 20)));
+    const uint64_t per = (bytes + nt - 1) / nt;
+    pool.run(nt, [&](unsigned t) {
+      const uint64_t lo = pos + t * per;
+      if (lo < end) copy_range(lo, std::min<uint64_t>(end, lo + per));
+    });
+    t_fill += std::chrono::duration<double>(clk::now() - t1).count();
+    HIP_TRY(hipMemcpyAsync(ddata + pos, st, bytes, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipEventRecord(stage_ev[gstage], stream));
+    gused[gstage] = true;
+    gstage = (gstage + 1) % nstages;
+    gpos = end;
+    return 0;
+  }
+
   // SHA-512[..32] of every batch of the group into out32 (32 bytes each)
   int digest_group(const std::vector<Item>& g, uint8_t* out32) {
     const size_t k = g.size();
@@ -175,11 +256,11 @@ struct Digester {
       return rc;
     }
     using clk = std::chrono::steady_clock;
-    double t_wait = 0, t_fill = 0;
     const auto t_start = clk::now();
     // mirror path: every batch in the receive arena, most of its bytes already on their way into
     // the arena's device mirror (stream_arena, queued while the group was collected): the kernel
-    // reads them in place there.  Otherwise the batches are gathered into the group's buffer.
+    // reads them in place there.  Otherwise the batches are gathered into the group's buffer, the
+    // stages not yet gathered while the group was collected now (gather_stage).
     const bool direct = mirrored;
     uint64_t total = 0;
     if (direct) {
@@ -191,54 +272,13 @@ struct Digester {
       ++direct_groups;
     } else {
       for (size_t i = 0; i < k; ++i) {
-        hse[i] = total;
-        hse[k + i] = total + g[i].len;
-        total += padded(g[i].len);
+        hse[i] = gstart[i];
+        hse[k + i] = gstart[i] + g[i].len;
       }
-      if (total + 16 > ddata_cap) {
-        if (ddata) HIP_TRY(hipFree(ddata));
-        ddata = nullptr;
-        ddata_cap = 0;
-        // headroom for slightly larger groups, but never past the per-launch cap
-        const size_t cap = std::max<size_t>(total + 16, std::min<size_t>((total + 16) + (total + 16) / 4, max_bytes + 16));
-        HIP_TRY(hipMalloc(&ddata, cap));
-        ddata_cap = cap;
-      }
-    }
-    // gather through the pinned stages: fill one (with copy_threads host threads, each a
-    // contiguous byte range of the stage) while the others' DMA is in flight.  Stage s covers the
-    // device layout's bytes [pos, pos + STAGE); batch i sits at hse[i] (16-byte aligned starts).
-    int s = 0;
-    bool used[MAX_STAGES] = {};
-    size_t first = 0;   // first batch that may overlap the current stage
-    for (uint64_t pos = 0; !direct && pos < total; pos += STAGE) {
-      const uint64_t end = std::min<uint64_t>(pos + STAGE, total);
-      const auto t0 = clk::now();
-      if (used[s]) HIP_TRY(hipEventSynchronize(stage_ev[s]));   // its previous DMA has landed
-      const auto t1 = clk::now();
-      t_wait += std::chrono::duration<double>(t1 - t0).count();
-      while (first < k && hse[k + first] <= pos) ++first;   // batches wholly in earlier stages
-      auto copy_range = [&](uint64_t lo, uint64_t hi) {
-        // batches overlapping [lo, hi), found from `first` (starts are ascending)
-        size_t i = first;
-        while (i < k && hse[k + i] <= lo) ++i;
-        for (; i < k && hse[i] < hi; ++i) {
-          const uint64_t a0 = std::max<uint64_t>(hse[i], lo), a1 = std::min<uint64_t>(hse[k + i], hi);
-          if (a1 > a0) std::memcpy(stage[s] + (a0 - pos), g[i].p + (a0 - hse[i]), a1 - a0);
-        }
-      };
-      const uint64_t bytes = end - pos;
-      const unsigned nt = (unsigned)std::min<uint64_t>(copy_threads, (bytes + (2u << 20) - 1) / (2u << 20));
-      const uint64_t per = (bytes + nt - 1) / nt;
-      pool.run(nt, [&](unsigned t) {
-        const uint64_t lo = pos + t * per;
-        if (lo < end) copy_range(lo, std::min<uint64_t>(end, lo + per));
-      });
-      t_fill += std::chrono::duration<double>(clk::now() - t1).count();
-      HIP_TRY(hipMemcpyAsync(ddata + pos, stage[s], bytes, hipMemcpyHostToDevice, stream));
-      HIP_TRY(hipEventRecord(stage_ev[s], stream));
-      used[s] = true;
-      s = (s + 1) % nstages;
+      total = gtotal;
+      if (int rc = ensure_ddata(total, false)) return rc;
+      while (gpos < total)
+        if (int rc = gather_stage(g, std::min<uint64_t>(gpos + STAGE, total))) return rc;
     }
     HIP_TRY(hipMemcpyAsync(dse, hse, 16 * k, hipMemcpyHostToDevice, stream));
     if (int rc = launch_digest(direct ? darena : ddata, dse, dse + k, k, dout, stream)) return rc;
@@ -278,6 +318,8 @@ struct Digester {
         mirrored_sent = 0;
         mirror_pending = g.back().len;
         mirror_runs = 0;
+        group_reset();
+        group_note(g.back());
         uint64_t gbytes = padded(g.back().len);
         t_group = std::chrono::steady_clock::now();
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
@@ -292,7 +334,14 @@ struct Digester {
           gbytes += padded(in.front().len);
           g.push_back(in.front());
           in.pop_front();
+          group_note(g.back());
           if (mirrored && !in_arena(g.back())) mirrored = false;   // a batch outside: gather the group
+          if (!mirrored && gtotal - gpos >= STAGE && !pending_err) {
+            // gather the stages whose batches have all arrived; the group stays open
+            lk.unlock();
+            while (!pending_err && gtotal - gpos >= STAGE) pending_err = gather_stage(g, gpos + STAGE);
+            lk.lock();
+          }
           if (mirrored && (mirror_pending += g.back().len) >= MIRROR_CHUNK && !pending_err) {
             // queue the DMAs of the arena batches collected so far; the group stays open
             lk.unlock();
