@@ -785,7 +785,7 @@ def cpu_digest_openssl(blob: bytes, nb: int, th: int, budget_s: float):
             "parity_ok": ok, "sample": "%d x %d cfg-4 batches (hashlib/OpenSSL SHA-512, %d threads, %.1f s)" % (reps, nb, th, dt)}
 
 
-def roofline_verify(vpc, n: int, kernel_ms: float, effective_tops: float):
+def roofline_verify(vpc, n: int, kernel_ms: float, effective_tops: float, clock=None):
     """k_verify's roofline entry.  achieved = the VALU lane-instructions one launch issues (this
     build's SQ_INSTS_VALU x 64 from the committed rocprofv3 pass, profiles/<round>/summary.json)
     over the launch's duration measured live with HIP events; peak = the guide's VALU issue rate.
@@ -809,6 +809,14 @@ def roofline_verify(vpc, n: int, kernel_ms: float, effective_tops: float):
     else:
         out.update({"achieved": None, "frac": None, "traffic": None,
                     "pmc_source": "profiles/%s/summary.json missing" % PROFILE_ROUND})
+    if clock:
+        # the shader clock this box held under the load, from the kernel's stamp build
+        # (nwc_diag_verify_clock): the issue rate the clock allows, and the fraction of it reached
+        out["clock_ghz"] = clock["clock_ghz"]
+        out["clock"] = dict(clock, source="k_verify stamp build: median over waves of d(s_memtime)/d(s_memrealtime) "
+                                          "x 100 MHz, one launch after ~2 s of back-to-back launches")
+        if out.get("achieved"):
+            out["frac_at_clock"] = out["achieved"] / (128 * 256 * clock["clock_ghz"] * 1e9 / 1e12)
     return out
 
 
@@ -912,6 +920,8 @@ def main():
     ap.add_argument("--cfg5-total", type=int, default=64 << 20, help="cfg 5 signatures over all ranks (0 = skip)")
     ap.add_argument("--host-digest-group", type=int, default=8192,
                     help="cfg 4 from host memory through nwc_digester: batches per group (0 = skip; needs --e2e-reps)")
+    ap.add_argument("--clock-s", type=float, default=2.0,
+                    help="seconds of back-to-back launches before the stamped clock launch (0 = skip)")
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="cfg 2 end to end through the host ABI from pageable host buffers (0 = skip)")
     args = ap.parse_args()
@@ -955,6 +965,17 @@ def main():
         ok = ok and bool(device.unpack_bits(allw, world * words.numel() * 64).all())
     value = world * n * args.steps / dt
     effective_tops = n / (kernel_ms * 1e-3) * ops_per_verify() / 1e12
+    # the clock the chip held under this load (MI355X_MICROARCH.md DVFS item 6): ~2 s more of
+    # back-to-back launches, then one launch of the kernel's stamp build (never the timed kernel)
+    clock = None
+    if args.clock_s > 0:
+        progress("headline: in-kernel clock")
+        reps = max(1, int(args.clock_s / max(kernel_ms * 1e-3, 1e-4)))
+        for _ in range(reps):
+            run()
+        ghz, waves = device.verify_clock(msgs, pks, sigs, words)
+        clock = {"clock_ghz": ghz, "waves": waves, "after_launches": reps,
+                 "ok": bool(device.unpack_bits(words, n).all())}
 
     # ---------------- digest leg (cfg 4)
     digest = None
@@ -1038,7 +1059,7 @@ def main():
                        "global_batch": world * n, "parallelism": "shard%d" % world,
                        "verdicts_ok": ok, "verdict_allgather_ms": gather_ms,
                        "allgather_needed": False},
-            "roofline": roofline_verify(vpc, n, kernel_ms, effective_tops),
+            "roofline": roofline_verify(vpc, n, kernel_ms, effective_tops, clock),
             "cpu_baseline": cpu,
             "digest": digest,
             "configs": extras,

@@ -73,6 +73,16 @@ int nwc_trim(void);
  * Not part of the crate's API. */
 int nwc_diag_set(const char* name, int64_t value);
 
+/* The shader clock the headline kernel holds under load: one launch of a diagnostic build of the
+ * strict verification kernel (k_verify with in-kernel stamps; the verdict path never runs it) on
+ * the caller's device inputs, as nwc_dev_verify(.., strict = 1, ..), synchronised on `stream`.
+ * Every wave stamps s_memtime / s_memrealtime at entry and exit; *clock_ghz = the median over
+ * waves of delta(memtime) / delta(realtime) x 100 MHz, *waves = the waves counted.  Call it after
+ * some seconds of back-to-back launches (MI355X_MICROARCH.md, DVFS item 6).  The verdict words
+ * are written as by nwc_dev_verify.  Diagnostics only, not part of the crate's API. */
+int nwc_diag_verify_clock(const void* d_msgs, uint64_t msg_stride, const void* d_pks, const void* d_sigs, uint64_t n,
+                          void* d_verdict_words, void* stream, double* clock_ghz, uint32_t* waves);
+
 /* ---- verification ----------------------------------------------------------------------- */
 /* crypto::Signature::verify -> dalek verify_strict.  Replaces crypto/src/lib.rs:200-204
  * (called from primary/src/messages.rs:63-66 Header::verify and :138-141 Vote::verify). */
@@ -126,8 +136,10 @@ int nwc_auto_cache_info(uint32_t* capacity, uint64_t* builds, uint64_t* hits);
  * committee cache samples its keys, and keys it repeats (>= ~1/4096 of the sample) join a
  * device-resident set with their flags and radix-2^14 combs (built once), so that votes of a
  * committee the caller never registered take the comb kernel -- cross-certificate key
- * aggregation, no nwc_set_committee needed.  Append-only up to `capacity` keys; emptied by
- * nwc_set_committee; NWC_LAUNCH_KEYS=0 (or nwc_diag_set("launch_keys", 0)) turns it off.
+ * aggregation, no nwc_set_committee needed.  Up to `capacity` keys; emptied by nwc_set_committee
+ * and nwc_trim, and replaced by a launch whose repeated keys do not fit while the held ones cover
+ * less than a quarter of its sample (a new committee); NWC_LAUNCH_KEYS=0 (or
+ * nwc_diag_set("launch_keys", 0)) turns it off.
  * Verdicts never depend on it.  Waits for the device.  Diagnostics only. */
 int nwc_launch_keys_info(uint32_t* held, uint32_t* capacity);
 

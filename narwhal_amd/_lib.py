@@ -34,6 +34,9 @@ _SIGS = {
     "nwc_memory_info": (ctypes.c_int, [ctypes.c_void_p]),
     "nwc_trim": (ctypes.c_int, []),
     "nwc_diag_set": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
+    "nwc_diag_verify_clock": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]),
     "nwc_verify_strict": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p]),
     "nwc_verify_batch": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p]),
     "nwc_verify_strict_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p]),

@@ -1114,6 +1114,7 @@ struct VerifyArgs {
   uint32_t force_fb_every;      // test hook: route equations i % every == 0 to the fallback (0 = off)
   Committee committee;          // n == 0: no cache
   uint32_t force_windows;       // test hook: run the half-size ladder with at least this many windows (0 = off)
+  uint64_t* stamps;             // k_verify<.., STAMP>: per wave {memtime, realtime} at entry and exit
 };
 // Extra arguments of the comb path (kept out of VerifyArgs so the headline kernel's argument
 // block and register allocation do not change).
@@ -1145,23 +1146,37 @@ __device__ __forceinline__ void stage_base_tables(const ge_niels* src, ge_niels*
 #ifndef NWC_VERIFY_WAVES_PER_SIMD
 #define NWC_VERIFY_WAVES_PER_SIMD 2
 #endif
-template <bool HALF, bool CACHE, bool LIST = false>
+// Persistent grid (launch_verify: NWC_VERIFY_GRID_MULT blocks per resident block slot): block b
+// takes the 256-lane tiles b, b + gridDim.x, ...; lane slot (blockIdx.x * 256 + threadIdx.x) of
+// `scratch` holds its two tables.  Waves taking 64-lane tiles from a counter instead measured 5 %
+// slower, with the tables per resident lane or per equation alike (profiles/r05/ab_verify_sched.txt).
+// STAMP (a diagnostic build, never the verdict path): every wave stores s_memtime / s_memrealtime
+// at entry and exit into a.stamps, so the host reads the shader clock held under the load.
+template <bool HALF, bool CACHE, bool LIST = false, bool STAMP = false>
 __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(VerifyArgs a, CombArgs ca) {
   // HALF: per-wave LDS-DMA staging of radix-2^24 basepoint entries (8 KB per wave);
   // full-length ladder: the radix-256 basepoint table (15.5 KB).
   __shared__ uint4 lds[HALF ? 4 * STAGE_U4_PER_WAVE + BASE_DIGIT_WORDS * 64 : 129 * 30 / 4];
   ge_niels* sB = reinterpret_cast<ge_niels*>(lds);
   if constexpr (!HALF) stage_base_tables(a.base_table, sB, 129);
+  uint64_t t_entry = 0, r_entry = 0;
+  if constexpr (STAMP) {
+    t_entry = __builtin_amdgcn_s_memtime();
+    r_entry = __builtin_amdgcn_s_memrealtime();
+  }
   uint4* stage = lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * STAGE_U4_PER_WAVE;
   const BaseDigits bd{reinterpret_cast<i32*>(lds + 4 * STAGE_U4_PER_WAVE) + threadIdx.x};
+  const uint64_t n = LIST ? (uint64_t)*ca.count : a.n;
+  const u32 lane = threadIdx.x & 63u;
   const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t* base = a.scratch + slot * 2 * TAB_BYTES_PER_LANE;
   const LaneTable ta{reinterpret_cast<uint4*>(base)};
   const LaneTable tr{reinterpret_cast<uint4*>(base + TAB_BYTES_PER_LANE)};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t n = LIST ? (uint64_t)*ca.count : a.n;
-  for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < n; b0 += stride) {
-    const uint64_t idx = b0 + threadIdx.x;
+  for (uint64_t bb = (uint64_t)blockIdx.x * blockDim.x; bb < n; bb += stride) {
+    const uint64_t b0 = bb + (threadIdx.x & ~63u);   // this wave's 64 equations
+    const u32 tile = (u32)(b0 >> 6);
+    const uint64_t idx = b0 + lane;
     const bool active = idx < n;
     const uint64_t i = LIST ? (active ? (uint64_t)ca.list[idx] : 0) : idx;
     u32 mw[8], aw[8], sgw[16];
@@ -1179,7 +1194,15 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
       if (v) atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));
     } else {
       const uint64_t ballot = __ballot(v);
-      if ((threadIdx.x & 63) == 0 && b0 + (threadIdx.x & ~63u) < n) a.out_bits[(b0 + threadIdx.x) >> 6] = ballot;
+      if (lane == 0 && b0 < n) a.out_bits[tile] = ballot;
+    }
+  }
+  if constexpr (STAMP) {
+    const uint64_t t_exit = __builtin_amdgcn_s_memtime();
+    const uint64_t r_exit = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+      uint64_t* w = a.stamps + 4 * ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+      w[0] = t_entry; w[1] = t_exit; w[2] = r_entry; w[3] = r_exit;
     }
   }
 }
@@ -1188,6 +1211,7 @@ template __global__ void k_verify<true, false>(VerifyArgs, CombArgs);
 template __global__ void k_verify<true, true>(VerifyArgs, CombArgs);
 template __global__ void k_verify<false, false>(VerifyArgs, CombArgs);
 template __global__ void k_verify<true, false, true>(VerifyArgs, CombArgs);
+template __global__ void k_verify<true, false, false, true>(VerifyArgs, CombArgs);
 
 // Full-length re-verification of the lanes k_verify could not reduce (rare); sets their bits.
 __global__ __launch_bounds__(256) void k_verify_fallback(VerifyArgs a) {

@@ -10,8 +10,9 @@
 // -- its flags (decodes, small order, 8-torsion) and its radix-2^14 comb, built once -- after which
 // the launch runs the committee comb kernel (k_verify_comb: 31 fixed-base additions per vote, no
 // decompression) over it, and the votes of other keys take the per-vote ladder in list mode.  The
-// set persists across launches (append-only, LK_MAX_KEYS keys; nwc_set_committee empties it), so a
-// node's steady state pays only the census.  Verdicts are those of the per-vote leaves: the key
+// set persists across launches (LK_MAX_KEYS keys; emptied by nwc_set_committee, by nwc_trim, and
+// by a launch whose repeated keys it no longer covers -- see k_lk_select), so a node's steady
+// state pays only the census.  Verdicts are those of the per-vote leaves: the key
 // set changes which kernel decides a vote, never the verdict (tests/test_gpu_launch_keys.py).
 //
 // The whole pipeline stays on the launch's stream (no host synchronisation): k_lk_select (one
@@ -48,17 +49,27 @@ __device__ __forceinline__ bool key_equal(const uint8_t* pks, u32 idx, const u32
 
 // One block of 1024 threads: LDS census of LK_SAMPLES equally spaced equations' keys, then the
 // keys with >= LK_MIN_HITS hits that the set does not hold yet join it (in census-slot order).
+// Replacement: when they do not all fit and the held keys cover less than a quarter of the
+// sample's repeated-key hits (the node's committee changed -- an epoch change -- or the set filled
+// with keys this traffic no longer carries), the set is emptied first and the launch's own
+// repeated keys join it.  A set that still covers its share of the traffic keeps its keys, and
+// the keys that do not fit take the per-vote ladder.
 __global__ __launch_bounds__(1024) void k_lk_select(const uint8_t* pks, uint64_t n, LaunchKeys lk) {
   constexpr u32 EMPTY = 0xFFFFFFFFu;
   __shared__ u32 cidx[LK_CENSUS];
   __shared__ u32 ccnt[LK_CENSUS];
   __shared__ u32 fresh[LK_MAX_KEYS];
-  __shared__ u32 nfresh;
+  __shared__ u32 nfresh, held_hits, fresh_hits, reset;
   for (u32 s = threadIdx.x; s < LK_CENSUS; s += blockDim.x) {
     cidx[s] = EMPTY;
     ccnt[s] = 0;
   }
-  if (threadIdx.x == 0) nfresh = 0;
+  if (threadIdx.x == 0) {
+    nfresh = 0;
+    held_hits = 0;
+    fresh_hits = 0;
+    reset = 0;
+  }
   __syncthreads();
   const uint64_t S = n < LK_SAMPLES ? n : LK_SAMPLES;
   for (uint64_t j = threadIdx.x; j < S; j += blockDim.x) {
@@ -76,18 +87,30 @@ __global__ __launch_bounds__(1024) void k_lk_select(const uint8_t* pks, uint64_t
     }
   }
   __syncthreads();
-  const u32 held = lk.state[0];
-  const Committee cur{lk.keys, lk.flags, nullptr, lk.comb, lk.slots, LK_SLOTS - 1, held};
+  const u32 held0 = lk.state[0];
+  const Committee cur{lk.keys, lk.flags, nullptr, lk.comb, lk.slots, LK_SLOTS - 1, held0};
   for (u32 s = threadIdx.x; s < LK_CENSUS; s += blockDim.x) {
     if (cidx[s] == EMPTY || ccnt[s] < LK_MIN_HITS) continue;
     u32 aw[8];
     load_words8(pks + 32 * (uint64_t)cidx[s], aw);
-    if (committee_lookup(cur, aw) >= 0) continue;
+    if (committee_lookup(cur, aw) >= 0) {
+      atomicAdd(&held_hits, ccnt[s]);
+      continue;
+    }
+    atomicAdd(&fresh_hits, ccnt[s]);
     const u32 k = atomicAdd(&nfresh, 1u);
-    if (held + k < LK_MAX_KEYS) fresh[k] = cidx[s];
+    if (k < LK_MAX_KEYS) fresh[k] = cidx[s];
   }
   __syncthreads();
+  if (threadIdx.x == 0) reset = (held0 + nfresh > LK_MAX_KEYS && 3u * held_hits < fresh_hits) ? 1u : 0u;
+  __syncthreads();
+  if (reset) {
+    // every launch that read the set is ordered before this one (the caller's scratch_free wait)
+    for (u32 s = threadIdx.x; s < LK_SLOTS; s += blockDim.x) lk.slots[s] = -1;
+    __syncthreads();
+  }
   if (threadIdx.x == 0) {
+    const u32 held = reset ? 0u : held0;
     const u32 add = min(nfresh, LK_MAX_KEYS - held);
     u32 q = held;
     for (u32 k = 0; k < add; ++k) {

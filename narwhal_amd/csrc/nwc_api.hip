@@ -135,6 +135,7 @@ struct DevCtx {
   size_t scratch_cap = 0;
   uint32_t* fb_list = nullptr;     // lanes whose half-size reduction failed (k_verify_fallback)
   uint32_t* fb_count = nullptr;
+  uint64_t* stamps = nullptr;      // k_verify<.., STAMP>: 4 words per wave of the resident grid (nwc_diag_verify_clock)
   size_t fb_cap = 0;
   hipEvent_t scratch_free = nullptr;
   // batch-leaf torsion post-pass (k_tors_*): key hash set sized for fb_cap equations
@@ -547,8 +548,48 @@ VPath verify_path() {
   return p;
 }
 
+// Device memory of the verification path (a primary and workers share the GPU:
+// worker/src/worker.rs:182,227).  One launch takes at most NWC_VERIFY_MAX_LAUNCH equations (larger
+// calls run as consecutive launches of that size, launch_verify), so the per-launch lists below are
+// bounded; and lists larger than NWC_VERIFY_KEEP_BYTES are shrunk to a smaller launch's size
+// when one comes (after the device has finished with them).  The per-lane table slots are sized
+// for the resident grid, not for n.
+#ifndef NWC_VERIFY_MAX_LAUNCH
+#define NWC_VERIFY_MAX_LAUNCH (16ull << 20)
+#endif
+uint64_t verify_max_launch() {
+  static const uint64_t m = [] {
+    const char* e = std::getenv("NWC_VERIFY_MAX_LAUNCH");
+    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : (uint64_t)NWC_VERIFY_MAX_LAUNCH;
+    return std::max<uint64_t>(1u << 16, v / 64 * 64);
+  }();
+  return m;
+}
+size_t verify_keep_bytes() {
+  static const size_t k = [] {
+    const char* e = std::getenv("NWC_VERIFY_KEEP_BYTES");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)256 << 20;
+  }();
+  return k;
+}
+// bytes of the per-launch lists: fb_list, uc_list, ts_uniq (4 B per entry) and the torsion hash set
+size_t list_bytes(uint64_t cap, uint64_t slots) { return 12 * (size_t)cap + 8 * (size_t)slots; }
+void free_lists(DevCtx& d) {
+  for (void* p : {(void*)d.fb_list, (void*)d.uc_list, (void*)d.ts_slots, (void*)d.ts_flag, (void*)d.ts_uniq})
+    if (p) (void)hipFree(p);
+  d.fb_list = nullptr;
+  d.uc_list = nullptr;
+  d.ts_slots = nullptr;
+  d.ts_flag = nullptr;
+  d.ts_uniq = nullptr;
+  d.fb_cap = 0;
+  d.ts_slot_count = 0;
+}
+
 int ensure_scratch(DevCtx& d, size_t bytes, uint64_t n) {
-  if (bytes <= d.scratch_cap && n <= d.fb_cap) return 0;
+  const uint64_t want = n + n / 2 + 4096;
+  const bool shrink = d.fb_cap > 4 * want && list_bytes(d.fb_cap, d.ts_slot_count) > verify_keep_bytes();
+  if (bytes <= d.scratch_cap && n <= d.fb_cap && !shrink) return 0;
   HIP_TRY(hipEventSynchronize(d.scratch_free));
   if (bytes > d.scratch_cap) {
     if (d.scratch) HIP_TRY(hipFree(d.scratch));
@@ -557,20 +598,9 @@ int ensure_scratch(DevCtx& d, size_t bytes, uint64_t n) {
     HIP_TRY(hipMalloc(&d.scratch, bytes));
     d.scratch_cap = bytes;
   }
-  if (n > d.fb_cap) {
-    if (d.fb_list) HIP_TRY(hipFree(d.fb_list));
-    if (d.uc_list) HIP_TRY(hipFree(d.uc_list));
-    if (d.ts_slots) HIP_TRY(hipFree(d.ts_slots));
-    if (d.ts_flag) HIP_TRY(hipFree(d.ts_flag));
-    if (d.ts_uniq) HIP_TRY(hipFree(d.ts_uniq));
-    d.fb_list = nullptr;
-    d.uc_list = nullptr;
-    d.ts_slots = nullptr;
-    d.ts_flag = nullptr;
-    d.ts_uniq = nullptr;
-    d.fb_cap = 0;
-    d.ts_slot_count = 0;
-    const size_t c = n + n / 2 + 4096;
+  if (shrink || n > d.fb_cap) {
+    free_lists(d);
+    const size_t c = want;
     HIP_TRY(hipMalloc(&d.fb_list, 4 * c));
     HIP_TRY(hipMalloc(&d.uc_list, 4 * c));
     // the hash set stays at most half full: >= 2 slots per equation
@@ -700,12 +730,27 @@ int ensure_stager(DevCtx& d) {
 
 // launch_verify flags: the caller checked on the host that every key is in the committee cache,
 // and/or out_words is already zero (both let the latency path run as a single kernel)
-constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4;   // LV_AUTO: the keys are in the auto cache
+// LV_AUTO: the keys are in the auto cache; LV_STAMP: the headline kernel's clock-stamp build
+// (k_verify<.., STAMP>, nwc_diag_verify_clock)
+constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4, LV_STAMP = 8;
 
 int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
                   hipStream_t s, int flags = 0, uint8_t* vbytes = nullptr) {
   if (n == 0) return 0;
+  if (n > verify_max_launch() && !vbytes) {
+    // consecutive launches of at most NWC_VERIFY_MAX_LAUNCH equations (a multiple of 64: whole
+    // verdict words), so the per-launch lists stay bounded; every equation is independent, so the
+    // verdicts are those of one launch (launch keys and the torsion set are per launch anyway)
+    const uint64_t step = verify_max_launch();
+    for (uint64_t lo = 0; lo < n; lo += step) {
+      const uint64_t len = std::min(step, n - lo);
+      if (int rc = launch_verify(d, msg_index ? msgs : msgs + 32 * lo * msg_stride, msg_index ? msg_index + lo : nullptr,
+                                 msg_stride, pks + 32 * lo, sigs + 64 * lo, len, strict, out_words + lo / 64, s, flags))
+        return rc;
+    }
+    return 0;
+  }
   // equation indices travel as uint32 (fallback / uncached / torsion lists)
   if (n > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "more than 2^32 - 1 equations in one launch");
   const VPath path = verify_path();
@@ -759,8 +804,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const uint64_t tiles = (n + 255) / 256;
   // persistent grid: a few blocks per resident slot so the tail is short
   const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * NWC_VERIFY_GRID_MULT;
-  const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
   size_t need = (size_t)cap * 256 * 2 * nwc::TAB_BYTES_PER_LANE;
+  const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
   // comb grid: at most the resident blocks; tile t goes to block t mod grid, so every lane gets
   // ceil or floor of n / lanes equations (in chunks of COMB_BATCH sharing one inversion), and
   // a small n spreads one equation per lane
@@ -789,6 +834,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
   a.force_windows = knobs().force_windows.load();
+  a.stamps = d.stamps;
   const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
   const bool half = path != VPath::Full;
   // small batch-leaf launches outside the comb path: the keys' torsion test (one long serial
@@ -814,21 +860,23 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
       hipLaunchKernelGGL(nwc::k_verify_comb, dim3(gridc), dim3(256), 0, s, a, ca);
     }
     HIP_TRY(hipGetLastError());
-    // uncached keys: half-size equations in list mode (blocks exit at once when the list is empty)
+    // uncached keys: half-size equations in list mode (waves exit at once when the list is empty)
     nwc::VerifyArgs l = a;
     l.committee.n = 0;
-    const unsigned lgrid = (unsigned)std::min<uint64_t>(grid, (uint64_t)d.cus * d.verify_blocks_per_cu);
-    hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3(lgrid), dim3(256), 0, s, l, ca);
-  } else if (half && cm.n) {
-    hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a, ca);
+    hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3(grid), dim3(256), 0, s, l, ca);
   } else if (cold) {
     if (!(flags & LV_OUT_ZEROED)) HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
     hipLaunchKernelGGL(nwc::k_verify_cold, dim3((unsigned)n), dim3(256), 0, s, a, (const nwc::ge_niels_pad*)d.comb16,
                        (uint8_t*)nullptr);
-  } else if (half) {
-    hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a, ca);
   } else {
-    hipLaunchKernelGGL((nwc::k_verify<false, false>), dim3(grid), dim3(256), 0, s, a, ca);
+    if (half && cm.n)
+      hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a, ca);
+    else if (half && (flags & LV_STAMP))
+      hipLaunchKernelGGL((nwc::k_verify<true, false, false, true>), dim3(grid), dim3(256), 0, s, a, ca);
+    else if (half)
+      hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a, ca);
+    else
+      hipLaunchKernelGGL((nwc::k_verify<false, false>), dim3(grid), dim3(256), 0, s, a, ca);
   }
   HIP_TRY(hipGetLastError());
   if (half) {
@@ -1174,7 +1222,15 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
 int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8_t* pks, const uint8_t* sigs,
                   uint64_t nvotes, uint64_t* leaf, hipStream_t s) {
   if (nvotes == 0) return 0;
-  if (nvotes > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "more than 2^32 - 1 votes in one call");
+  if (nvotes > verify_max_launch()) {
+    // consecutive launches of at most NWC_VERIFY_MAX_LAUNCH votes, as launch_verify: sub-batches
+    // are any consecutive votes (each reads its own certificate's digest through mi)
+    const uint64_t step = verify_max_launch();
+    for (uint64_t lo = 0; lo < nvotes; lo += step)
+      if (int rc = launch_straus(d, dig, mi + lo, pks + 32 * lo, sigs + 64 * lo, std::min(step, nvotes - lo), leaf + lo / 64, s))
+        return rc;
+    return 0;
+  }
   if (!d.comb16)   // no basepoint comb (NWC_COMB16=0): the exact leaves
     return launch_verify(d, dig, mi, 0, pks, sigs, nvotes, 0, leaf, s);
   // sub-batches of ~12 votes (knobs().straus_nq), every lane slot the same number of rounds
@@ -1210,8 +1266,8 @@ int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8
   HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(nwc::k_verify_straus, dim3((unsigned)(lanes / 256)), dim3(256), 0, s, sa);
   HIP_TRY(hipGetLastError());
-  const nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
-                          d.fb_count, 0u, nwc::Committee{}};
+  nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
+                    d.fb_count, 0u, nwc::Committee{}};
   const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
   hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3((unsigned)lgrid), dim3(256), 0, s, a, ca);
   HIP_TRY(hipGetLastError());
@@ -1368,6 +1424,13 @@ int nwc_init(uint32_t device_mask) {
     g_devs.push_back(std::move(d));
   }
   if (g_devs.empty()) return set_err(NWC_ERR_NO_DEVICE, "device mask 0x%x selects no visible device", device_mask);
+  // A process that exits without nwc_shutdown (a Python caller, a node killed by its runtime)
+  // still releases every device object of the library -- streams synchronised, copies finished,
+  // pinned stages and HBM freed -- before the HIP runtime's own exit-time teardown: atexit
+  // handlers run in reverse order of registration, and this one is registered after the runtime
+  // was initialised above.  nwc_shutdown is idempotent (the second call finds no context).
+  static const bool at_exit = std::atexit([] { nwc_shutdown(); }) == 0;
+  (void)at_exit;
   // Test hook: NWC_VIRTUAL_DEVICES=k opens k contexts (own stream, tables, buffers) on a single
   // selected GPU, so the multi-device host paths -- shard threads, certificate cuts, bitmap
   // merges -- run for real on a one-GPU box (tests/test_gpu_multidev.py).
@@ -1393,6 +1456,7 @@ void nwc_shutdown(void) {
     if (d->scratch) (void)hipFree(d->scratch);
     if (d->fb_list) (void)hipFree(d->fb_list);
     if (d->fb_count) (void)hipFree(d->fb_count);
+    if (d->stamps) (void)hipFree(d->stamps);
     if (d->cm_keys) (void)hipFree(d->cm_keys);
     if (d->cm_flags) (void)hipFree(d->cm_flags);
     if (d->cm_tables) (void)hipFree(d->cm_tables);
@@ -1745,6 +1809,34 @@ int nwc_dev_verify(const void* d_msgs, const void* d_msg_index, uint64_t msg_str
   if (n && (!d_msgs || !d_pks || !d_sigs || !d_verdict_words)) return set_err(NWC_ERR_ARG, "null buffer");
   return launch_verify(d, (const uint8_t*)d_msgs, (const uint32_t*)d_msg_index, msg_stride, (const uint8_t*)d_pks,
                        (const uint8_t*)d_sigs, n, strict, (uint64_t*)d_verdict_words, s);
+}
+
+int nwc_diag_verify_clock(const void* d_msgs, uint64_t msg_stride, const void* d_pks, const void* d_sigs, uint64_t n,
+                          void* d_verdict_words, void* stream, double* clock_ghz, uint32_t* waves) {
+  DEV_PROLOGUE
+  if (!d_msgs || !d_pks || !d_sigs || !d_verdict_words || !clock_ghz) return set_err(NWC_ERR_ARG, "null buffer");
+  if (n < 4096) return set_err(NWC_ERR_ARG, "the clock stamp needs a full launch (n >= 4096)");
+  // one stamp slot per wave of the largest grid launch_verify gives k_verify
+  const uint64_t nwaves = (uint64_t)d.cus * d.verify_blocks_per_cu * NWC_VERIFY_GRID_MULT * 4;
+  if (!d.stamps) HIP_TRY(hipMalloc(&d.stamps, 32 * nwaves));
+  HIP_TRY(hipMemsetAsync(d.stamps, 0, 32 * nwaves, s));
+  if (int rc = launch_verify(d, (const uint8_t*)d_msgs, nullptr, msg_stride, (const uint8_t*)d_pks, (const uint8_t*)d_sigs,
+                             n, 1, (uint64_t*)d_verdict_words, s, LV_STAMP))
+    return rc;
+  std::vector<uint64_t> st(4 * nwaves);
+  HIP_TRY(hipMemcpyAsync(st.data(), d.stamps, 32 * nwaves, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::vector<double> ghz;
+  for (uint64_t w = 0; w < nwaves; ++w) {
+    const uint64_t* x = &st[4 * w];
+    // a wave that ran at least ~10 us of real time (100 MHz ticks)
+    if (x[3] > x[2] + 1000 && x[1] > x[0]) ghz.push_back((double)(x[1] - x[0]) / (double)(x[3] - x[2]) * 0.1);
+  }
+  if (ghz.empty()) return set_err(NWC_ERR_DEVICE, "no wave stamped its clock");
+  std::nth_element(ghz.begin(), ghz.begin() + ghz.size() / 2, ghz.end());
+  *clock_ghz = ghz[ghz.size() / 2];
+  if (waves) *waves = (uint32_t)ghz.size();
+  return 0;
 }
 
 int nwc_dev_cert_reduce(const void* d_leaf_words, const void* d_offsets, uint64_t m, uint64_t nvotes,
@@ -2153,6 +2245,16 @@ int nwc_trim(void) {
   d.straus_scratch = nullptr; d.straus_cap = 0;
   d.arena = nullptr; d.arena_cap = 0;
   d.msg_arena = nullptr; d.msg_arena_cap = 0;
+  // the per-launch lists (fallback, uncached, torsion hash set) and the launch-key set (2.6 GB of
+  // combs): the next launch that needs them allocates them again, the launch keys empty
+  free_lists(d);
+  if (d.lk_alloc) {
+    for (void* p : {(void*)d.lk.keys, (void*)d.lk.flags, (void*)d.lk.slots, (void*)d.lk.comb, (void*)d.lk.bases,
+                    (void*)d.lk.state})
+      HIP_TRY(hipFree(p));
+    d.lk = nwc::LaunchKeys{};
+    d.lk_alloc = false;
+  }
   return 0;
 }
 

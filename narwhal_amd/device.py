@@ -48,6 +48,18 @@ def verify(msgs: torch.Tensor, pks: torch.Tensor, sigs: torch.Tensor, strict: bo
     return out
 
 
+def verify_clock(msgs: torch.Tensor, pks: torch.Tensor, sigs: torch.Tensor, out: torch.Tensor) -> Tuple[float, int]:
+    """nwc_diag_verify_clock: one stamped launch of the strict kernel over these inputs; returns the
+    median in-kernel shader clock (GHz) over waves and the number of waves. Synchronises."""
+    lib = _lib.load()
+    n = pks.shape[0]
+    ghz = ctypes.c_double()
+    waves = ctypes.c_uint32()
+    _lib.check(lib.nwc_diag_verify_clock(_ptr(msgs), 1, _ptr(pks), _ptr(sigs), n, _ptr(out), _stream(),
+                                         ctypes.byref(ghz), ctypes.byref(waves)))
+    return ghz.value, waves.value
+
+
 def verify_batch_straus(digests: torch.Tensor, offsets: torch.Tensor, msg_index: torch.Tensor, pks: torch.Tensor,
                         sigs: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dalek's batch equation over sub-batches of ~12 votes (Straus per lane), the exact leaves for

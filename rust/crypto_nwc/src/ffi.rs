@@ -32,6 +32,9 @@ extern "C" {
     pub fn nwc_memory_info(out: *mut nwc_memory) -> c_int;
     pub fn nwc_trim() -> c_int;
     pub fn nwc_diag_set(name: *const c_char, value: i64) -> c_int;
+    pub fn nwc_diag_verify_clock(d_msgs: *const c_void, msg_stride: u64, d_pks: *const c_void, d_sigs: *const c_void,
+                                 n: u64, d_verdict_words: *mut c_void, stream: *mut c_void, clock_ghz: *mut f64,
+                                 waves: *mut u32) -> c_int;
 
     pub fn nwc_verify_strict(msg32: *const u8, pk: *const u8, sig: *const u8) -> c_int;
     pub fn nwc_verify_batch(msg32: *const u8, pks: *const u8, sigs: *const u8, n: usize, bad_bitmap: *mut u8) -> c_int;

@@ -37,14 +37,21 @@ def build_abi_host() -> str:
     if _stale(ASAN_LIB, nb.sources()):
         subprocess.run([nb.HIPCC, "--offload-arch=gfx950", "-O2", "-g", "-std=c++20", "-fPIC", "-shared",
                         "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
-                        "-Xarch_host", "-fno-sanitize-recover=undefined", inc, "-I" + nb.CSRC,
+                        "-Xarch_host", "-fno-sanitize-recover=undefined", "-Xarch_host", "-fno-omit-frame-pointer",
+                        inc, "-I" + nb.CSRC,
                         "-o", ASAN_LIB + ".tmp", os.path.join(nb.CSRC, "nwc_api.hip")], check=True)
         os.replace(ASAN_LIB + ".tmp", ASAN_LIB)
     if _stale(ASAN_BIN, [src, ASAN_LIB]):
-        subprocess.run(["/opt/rocm/llvm/bin/clang", "-O1", "-g", "-fsanitize=address,undefined",
-                        "-fno-sanitize-recover=undefined", inc, src, "-L" + os.path.dirname(ASAN_LIB),
-                        "-l:" + os.path.basename(ASAN_LIB), "-lpthread", "-Wl,-rpath,$ORIGIN", "-o", ASAN_BIN],
+        # compiled as C, linked by clang++: the sanitizer runtime's own operator new / delete then
+        # serve libnwc's C++ allocations, so a leak report's stack (fast frame-pointer unwind)
+        # reaches libnwc's frames instead of stopping inside libstdc++'s operator new
+        obj = ASAN_BIN + ".o"
+        subprocess.run(["/opt/rocm/llvm/bin/clang", "-c", "-O1", "-g", "-fno-omit-frame-pointer",
+                        "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", inc, src, "-o", obj],
                        check=True)
+        subprocess.run(["/opt/rocm/llvm/bin/clang++", "-fsanitize=address,undefined", obj,
+                        "-L" + os.path.dirname(ASAN_LIB), "-l:" + os.path.basename(ASAN_LIB), "-lpthread",
+                        "-Wl,-rpath,$ORIGIN", "-o", ASAN_BIN], check=True)
     return BIN
 
 
@@ -96,6 +103,16 @@ def _keep_report(name, r):
             f.write(r.stdout)
     except OSError:
         pass
+
+
+def asan_env(**extra):
+    """The sanitized host's environment: leak checking on (the C host calls
+    __lsan_do_recoverable_leak_check after nwc_shutdown; suppressions for the ROCm runtime's frames
+    only, tests/cpp/lsan.supp), UBSan fatal with stacks, three virtual device contexts."""
+    supp = os.path.join(ROOT, "tests", "cpp", "lsan.supp")
+    return dict(os.environ, NWC_VIRTUAL_DEVICES="3", ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0:malloc_context_size=40",
+                LSAN_OPTIONS="suppressions=%s:print_suppressions=1" % supp,
+                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1", **extra)
 
 
 def test_c_host_under_asan(oracle, golden_verify, golden_batch):
@@ -168,13 +185,15 @@ def test_c_host_under_asan(oracle, golden_verify, golden_batch):
         want.append("G 0")
     lines.append("Y 4 2")
     want.append("Y 0")
-    env = dict(os.environ, NWC_VIRTUAL_DEVICES="3", ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0",
-               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    env = asan_env()
     r = subprocess.run([ASAN_BIN], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=600, env=env)
     if r.returncode != 0:
         _keep_report("abi_host_asan", r)
     assert r.returncode == 0, (r.returncode, r.stdout[-500:], _report_head(r.stderr))
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+    assert "LeakSanitizer" not in r.stderr and "leaks after nwc_shutdown" not in r.stderr, _report_head(r.stderr)
+    # the leak check ran: LSan prints the suppressions it matched (the ROCm runtime's, if any)
+    print(r.stderr[-2000:])
     got = [l.rstrip() for l in r.stdout.splitlines()]
     assert len(got) == len(want), (len(got), len(want), r.stderr[-1000:])
     mism = [(i, g[:80], str(w)[:80]) for i, (g, w) in enumerate(zip(got, want)) if not _same(g, w)]

@@ -95,6 +95,30 @@ def test_set_fills_and_other_committees_take_the_ladder(oracle):
     assert _held(lib)[0] == 0
 
 
+def test_new_committee_replaces_the_set(oracle):
+    """Two disjoint 100-key committees in turn (an epoch change): the second one's launch finds
+    the held keys covering none of its repeated-key sample and no room for its own, so the set is
+    emptied and the second committee's keys join; then the first committee comes back and takes
+    the set again.  Verdicts equal the oracle's leaves throughout."""
+    from narwhal_amd import _lib
+    lib = _lib.load()
+    _lib.check(lib.nwc_set_committee(None, 0))
+    rng = np.random.default_rng(74)
+    c1 = _committee_workload(oracle, rng, 100, 80_000)
+    c2 = _committee_workload(oracle, rng, 100, 80_000)
+    keys1 = {bytes(k) for k in c1[1]}
+    for work, name in ((c1, "first"), (c2, "second"), (c1, "first again")):
+        exp = oracle.leaf_many(*work)
+        got = _leaf(*work)
+        held, cap = _held(lib)
+        assert held == 100, (name, held)
+        assert (got == exp).all(), (name, np.nonzero(got != exp)[0][:10])
+        again = _leaf(*work)                      # steady state over the replaced set
+        assert (again == exp).all() and _held(lib)[0] == 100, name
+    assert len(keys1 & {bytes(k) for k in c2[1]}) == 0
+    _lib.check(lib.nwc_set_committee(None, 0))
+
+
 def test_golden_keys_repeated_join_with_their_flags(golden_verify, oracle):
     """Every golden strict/leaf case (undecodable keys, small-order keys, keys with an 8-torsion
     component, non-canonical encodings, s >= l, ...) tiled 600 times: their keys are frequent, so

@@ -132,21 +132,79 @@ def test_failed_group_returns_its_tags():
             dg.close()   # destroy reports the sticky error
 
 
+def _tiled_triples(n: int, base: int = 1 << 14, tag: bytes = b"mem"):
+    """n triples tiled from `base` GPU-signed ones, every 7th of the base corrupted (expected
+    verdicts known by construction: equation i is valid iff (i mod base) % 7 != 0)."""
+    from narwhal_amd import device
+    msgs = device.derive32(tag + b"-msg", 0, base)
+    pks, sigs = device.keygen_sign(device.derive32(tag + b"-seed", 0, base), msgs)
+    sigs[::7, 40] ^= 1
+    reps = (n + base - 1) // base
+    t = lambda x: x.repeat(reps, 1)[:n].contiguous()  # noqa: E731
+    return t(msgs), t(pks), t(sigs)
+
+
 def test_trim_releases_scratch():
-    """nwc_trim frees the on-demand scratch; the next call re-allocates it and verdicts hold."""
+    """nwc_trim frees the on-demand scratch -- table slots, arenas, the per-launch lists and the
+    launch-key set -- down to nothing; the next call re-allocates what it needs and verdicts hold."""
     import torch
     from narwhal_amd import _lib, device
-    n = 1 << 15
-    msgs = device.derive32(b"trim-msg", 0, n)
-    pks, sigs = device.keygen_sign(device.derive32(b"trim-seed", 0, n), msgs)
-    sigs[::7, 40] ^= 1
+    n = 1 << 17
+    msgs, pks, sigs = _tiled_triples(n, 1 << 12, b"trim")
     first = device.unpack_bits(device.verify(msgs, pks, sigs, strict=True), n)
+    leaf = device.unpack_bits(device.verify(msgs, pks, sigs, strict=False), n)   # launch keys join
     torch.cuda.synchronize()
     before = _lib.memory_info()
     assert before["scratch"] > 0 and before["tables"] > (2 << 30)
     _lib.check(_lib.load().nwc_trim())
     after = _lib.memory_info()
-    assert after["scratch"] < before["scratch"] and after["tables"] == before["tables"]
+    assert after["scratch"] == 0, after
+    assert after["tables"] == before["tables"] and after["auto_cache"] < before["auto_cache"]
     again = device.unpack_bits(device.verify(msgs, pks, sigs, strict=True), n)
+    leaf2 = device.unpack_bits(device.verify(msgs, pks, sigs, strict=False), n)
     torch.cuda.synchronize()
-    assert (again == first).all() and first.sum() == n - (n + 6) // 7
+    exp = (np.arange(n) % (1 << 12)) % 7 != 0
+    assert (first == exp).all() and (again == exp).all() and (leaf == exp).all() and (leaf2 == exp).all()
+
+
+def test_verify_memory_is_bounded_after_a_huge_launch():
+    """A 64M-equation launch runs as launches of at most NWC_VERIFY_MAX_LAUNCH (16M) equations, so
+    its lists are a 16M launch's; the next 1M launch shrinks lists above NWC_VERIFY_KEEP_BYTES
+    (256 MB) back to its own size.  Verdicts equal the construction in both."""
+    import torch
+    from narwhal_amd import _lib, device
+    lib = _lib.load()
+    _lib.check(lib.nwc_trim())
+    n = 64 << 20
+    msgs, pks, sigs = _tiled_triples(n)
+    words = device.verify(msgs, pks, sigs, strict=True)
+    torch.cuda.synchronize()
+    exp_base = (np.arange(1 << 14) % 7) != 0
+    got = device.unpack_bits(words, n)
+    assert (got.reshape(-1, 1 << 14) == exp_base).all()
+    big = _lib.memory_info()["scratch"]
+    # table slots of the resident grid (~302 MB) + lists for one 16M launch (~0.8 GB), not 64M's
+    assert big < (1400 << 20), big
+    del words
+    m = 1 << 20
+    small = device.unpack_bits(device.verify(msgs[:m], pks[:m], sigs[:m], strict=True), m)
+    torch.cuda.synchronize()
+    assert (small == np.tile(exp_base, m >> 14)).all()
+    after = _lib.memory_info()["scratch"]
+    assert after < big and after < (302 << 20) + (256 << 20), (big, after)
+    print("verify scratch after 64M: %.0f MB, after 1M: %.0f MB" % (big / 2**20, after / 2**20))
+
+
+def test_stamped_clock_launch():
+    """nwc_diag_verify_clock: the stamp build of the strict kernel returns a plausible shader
+    clock and the same verdicts as the verdict kernel."""
+    import torch
+    from narwhal_amd import device
+    n = 1 << 18
+    msgs, pks, sigs = _tiled_triples(n, 1 << 12, b"clock")
+    words = torch.empty(device.words_for(n), dtype=torch.int64, device="cuda")
+    ghz, waves = device.verify_clock(msgs, pks, sigs, words)
+    assert 0.5 < ghz < 3.0 and waves >= 1000, (ghz, waves)
+    exp = (np.arange(n) % (1 << 12)) % 7 != 0
+    assert (device.unpack_bits(words, n) == exp).all()
+    print("in-kernel clock %.3f GHz over %d waves" % (ghz, waves))

@@ -15,7 +15,7 @@ FFI = os.path.join(ROOT, "rust", "crypto_nwc", "src", "ffi.rs")
 # C parameter type -> Rust FFI type
 C2RUST = {
     "const uint8_t*": "*const u8", "uint8_t*": "*mut u8", "const uint32_t*": "*const u32",
-    "const uint64_t*": "*const u64", "uint64_t*": "*mut u64", "uint32_t*": "*mut u32", "int32_t*": "*mut i32",
+    "const uint64_t*": "*const u64", "uint64_t*": "*mut u64", "uint32_t*": "*mut u32", "int32_t*": "*mut i32", "double*": "*mut f64",
     "const void*": "*const c_void", "void*": "*mut c_void", "const char*": "*const c_char",
     "nwc_digester*": "*mut nwc_digester", "nwc_memory*": "*mut nwc_memory", "int64_t": "i64", "size_t*": "*mut usize", "size_t": "usize", "uint32_t": "u32", "uint64_t": "u64", "int": "c_int", "void": None,
 }

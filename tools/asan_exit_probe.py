@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Probe of the sanitized C host's exit path (VERDICT r04 "what's weak" #5): run
+tests/cpp/build/abi_host_asan on the golden batches, a sharded strict request, certificates and
+a digester group, leaving through main's return (NWC_HOST_EXIT=return: exit() with the atexit
+handlers, libnwc's static destructors and the HIP/HSA runtime's own teardown) instead of _exit.
+Every run's stderr is kept under gpurun_out/asan_exit_<k>.stderr; the summary line per run says
+whether ASan reported, and the frames of the first report are printed.
+
+    python tools/asan_exit_probe.py [runs]
+"""
+import json
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def requests():
+    from tests.oracle_lib import load_oracle
+    import numpy as np
+    orc = load_oracle()
+    gb = json.load(open(os.path.join(ROOT, "tests", "golden", "ed25519_batch.json")))
+    lines = []
+    for b in gb:
+        n = len(b["votes"])
+        lines.append("B %s %d %s" % (b["msg"], n, " ".join("%s %s" % (p, s) for p, s in b["votes"])))
+    rng = np.random.default_rng(5)
+    n = 9001
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pks, sigs = orc.keygen_sign_many(seeds, msgs)
+    lines.append("V %d" % n)
+    lines += ["%s %s %s" % (m.tobytes().hex(), p.tobytes().hex(), s.tobytes().hex()) for m, p, s in zip(msgs, pks, sigs)]
+    lines.append("W 40")
+    batches = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in rng.integers(1, 100_000, 30)]
+    lines.append("G 64 100000 1 %d" % len(batches))
+    lines += [b.hex() for b in batches]
+    lines.append("X 4 2")
+    return "\n".join(lines) + "\n"
+
+
+def main():
+    runs = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    from tests.test_gpu_abi_host import ASAN_BIN, asan_env
+    inp = requests()
+    out_dir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out_dir, exist_ok=True)
+    first = None
+    for k in range(runs):
+        r = subprocess.run([ASAN_BIN], input=inp, capture_output=True, text=True, timeout=300,
+                           env=asan_env(NWC_HOST_EXIT="return"))
+        open(os.path.join(out_dir, "asan_exit_%d.stderr" % k), "w").write(r.stderr)
+        rep = "==ERROR" in r.stderr or "CHECK failed" in r.stderr or "AddressSanitizer" in r.stderr
+        print("run %d: rc %d, sanitizer report: %s, lines out %d" % (k, r.returncode, rep, len(r.stdout.splitlines())),
+              flush=True)
+        if rep and first is None:
+            first = r.stderr
+    if first:
+        i = max(first.find("CHECK failed"), first.find("==ERROR"))
+        print(first[max(0, i - 300):i + 6000])
+        frames = re.findall(r"#\d+ 0x[0-9a-f]+ in (\S+) (\S+)", first)
+        print("frames:", frames[:40])
+
+
+if __name__ == "__main__":
+    main()
