@@ -82,6 +82,19 @@ def profile_counters(*kernel_names: str):
     return None
 
 
+CENSUS = os.path.join(ROOT, "profiles", "r05", "isa_census.json")   # tools/isa_census.py of this build
+
+
+def issue_cycles(kernel: str):
+    """Average issue cycles per wave64 VALU instruction of `kernel` (VOP3/VOP3P 4, VOP1/VOP2 2),
+    from the committed ISA census (static counts x trip counts, tools/isa_census.py)."""
+    try:
+        k = json.load(open(CENSUS))["kernels"][kernel]
+        return k["avg_issue_cycles"], k["share_4cycle"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
 def ops_per_verify() -> float:
     return W_S * OPS_S + W_M * OPS_M + W_SHA * OPS_SHA
 
@@ -320,8 +333,31 @@ def cpu_baseline_cfg1(d: bytes, p: bytes, s: bytes, n: int, calls: int):
         if i >= 20:
             lat.append(dt)
     lat = np.array(lat) * 1e6
-    return {"p50_us": float(np.percentile(lat, 50)), "p99_us": float(np.percentile(lat, 99)), "cores": 1,
-            "kind": "port", "sample": "%d calls, C restatement of dalek verify_batch (Straus), 1 thread" % calls}
+    out = {"p50_us": float(np.percentile(lat, 50)), "p99_us": float(np.percentile(lat, 99)), "cores": 1,
+           "kind": "port", "sample": "%d calls, C restatement of dalek verify_batch (Straus), 1 thread" % calls}
+    # also throughput over independent calls on every CPU the box grants
+    # (rayon-style, one certificate per task): the same certificate as k independent calls
+    from tests.oracle_lib import load_oracle
+    th = cpu_threads()
+    k = 256 * th
+    dg = np.frombuffer(d, np.uint8)[None, :].repeat(k, axis=0)
+    pk = np.frombuffer(p, np.uint8).reshape(n, 32)
+    sg = np.frombuffer(s, np.uint8).reshape(n, 64)
+    offs = (np.arange(k + 1) * n).astype(np.uint32)
+    P, S = np.ascontiguousarray(np.tile(pk, (k, 1))), np.ascontiguousarray(np.tile(sg, (k, 1)))
+    orc2 = load_oracle()
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        ok = orc2.batch_straus_many(dg, offs, P, S, threads=th)
+        reps += 1
+        if time.perf_counter() - t0 > 2.0:
+            break
+    dt = time.perf_counter() - t0
+    out["throughput"] = {"calls_per_s": reps * k / dt, "cores": th, "parity_ok": bool(ok.all()),
+                         "sample": "%d x %d independent verify_batch calls of the 3-vote certificate, %d threads, %.1f s"
+                                   % (reps, k, th, dt)}
+    return out
 
 
 def cpu_baseline_cfg3(cdig, pks, sigs, m: int, Q: int, bad, budget_s: float):
@@ -568,7 +604,7 @@ def bench_cfg3_wire(lib, m: int, steps: int):
             "host_abi_certs_per_s": m / hdt, "failing_certs": int(exp_bad.sum())}
 
 
-def bench_cfg5(lib, rank: int, world: int, total: int, steps: int):
+def bench_cfg5(lib, rank: int, world: int, total: int, steps: int, cpu_budget: float = 0.0):
     """BASELINE config 5: `total` (64M) signatures sharded in contiguous ranges of total/world over
     the ranks (strong scaling), 99 % honest-valid (cfg-2 seed scheme on the global index) and 1 %
     edge cases spread evenly over the golden edge-case classes (tests/golden/ed25519_verify.json:
@@ -629,11 +665,32 @@ def bench_cfg5(lib, rank: int, world: int, total: int, steps: int):
         import torch.distributed as dist
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
     del host_words
-    return {"workload": "cfg5: %d signatures (1%% edge cases over %d golden classes) sharded %d ways, verify_strict"
-                        % (total, len(edge), world),
-            "verifies_per_s": total / dt, "ms_per_pass": dt * 1e3, "per_gpu": per, "scaling": "strong",
-            "verdict_allgather_ms": gather_ms, "verdict_d2h_ms": d2h_ms, "allgather_needed": False,
-            "edge_slots_per_gpu": int(slot.numel()), "parity_ok": bool(okt.item() == 1)}
+    out = {"workload": "cfg5: %d signatures (1%% edge cases over %d golden classes) sharded %d ways, verify_strict"
+                       % (total, len(edge), world),
+           "verifies_per_s": total / dt, "ms_per_pass": dt * 1e3, "per_gpu": per, "scaling": "strong",
+           "verdict_allgather_ms": gather_ms, "verdict_d2h_ms": d2h_ms, "allgather_needed": False,
+           "edge_slots_per_gpu": int(slot.numel()), "parity_ok": bool(okt.item() == 1)}
+    if cpu_budget > 0 and rank == 0 and world == 1:
+        # the restatement's verify_strict on every CPU the box grants, on a
+        # prefix of the same mixed signatures (edge cases included), verdicts checked
+        from tests.oracle_lib import load_oracle
+        orc = load_oracle()
+        th = cpu_threads()
+        k = 4096 * th
+        while True:
+            m_, p_, s_ = (t[:k].cpu().numpy() for t in (msgs, pks, sigs))
+            t0 = time.perf_counter()
+            v = orc.strict_many(m_, p_, s_, th)
+            cdt = time.perf_counter() - t0
+            if cdt > cpu_budget / 4 or k >= per:
+                break
+            k = min(per, int(k * max(2.0, cpu_budget / max(cdt, 1e-3) * 0.8)))
+        out["cpu_baseline"] = {"value": k / cdt, "unit": "verifies/s", "cores": th, "kind": "port",
+                               "value_per_thread": k / cdt / th,
+                               "parity_ok": bool((v == expected[:k].cpu().numpy()).all()),
+                               "sample": "first %d of the cfg-5 signatures (%d edge cases; C restatement of dalek "
+                                         "verify_strict, %d threads, %.1f s)" % (k, int((gidx[:k] % 100 == 37).sum()), th, cdt)}
+    return out
 
 
 # ---- host ------------------------------------------------------------------------------------
@@ -809,6 +866,13 @@ def roofline_verify(vpc, n: int, kernel_ms: float, effective_tops: float, clock=
     else:
         out.update({"achieved": None, "frac": None, "traffic": None,
                     "pmc_source": "profiles/%s/summary.json missing" % PROFILE_ROUND})
+    cyc, share = issue_cycles("k_verify")
+    if cyc and out.get("frac"):
+        # the true issue fraction: every wave instruction priced at its own class's issue cycles
+        # (frac prices them all at 2, frac_vop3_rate all at 4); SIMD cycles at the 2.4 GHz peak
+        out["frac_issue"] = out["frac"] * cyc / 2
+        out["issue_census"] = {"avg_issue_cycles": cyc, "share_4cycle": share,
+                               "source": os.path.relpath(CENSUS, ROOT) + " (tools/isa_census.py)"}
     if clock:
         # the shader clock this box held under the load, from the kernel's stamp build
         # (nwc_diag_verify_clock): the issue rate the clock allows, and the fraction of it reached
@@ -817,6 +881,8 @@ def roofline_verify(vpc, n: int, kernel_ms: float, effective_tops: float, clock=
                                           "x 100 MHz, one launch after ~2 s of back-to-back launches")
         if out.get("achieved"):
             out["frac_at_clock"] = out["achieved"] / (128 * 256 * clock["clock_ghz"] * 1e9 / 1e12)
+            if out.get("frac_issue"):
+                out["frac_issue_at_clock"] = out["frac_issue"] * 2.4 / clock["clock_ghz"]
     return out
 
 
@@ -1024,7 +1090,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             extras["cfg4_host"] = {"error": repr(e)}
     if args.cfg5_total > 0:
-        extras["cfg5"] = bench_cfg5(lib, rank, world, args.cfg5_total, 2)
+        extras["cfg5"] = bench_cfg5(lib, rank, world, args.cfg5_total, 2, args.cpu_budget / 2)
     if world == 1 and args.cfg3_certs > 0:
         extras["cfg3"] = bench_cfg3(lib, args.cfg3_certs, max(1, args.steps // 2),
                                     args.cpu_budget / 2 if rank == 0 else 0.0)
@@ -1047,6 +1113,9 @@ def main():
         # counter fraction: this build's VALU lane-ops per launch (PMC) over the live kernel time
         digest["valu_frac"] = dpc["lane_ops_per_launch"] / (digest["kernel_ms"] * 1e-3) / (VALU_PEAK_TOPS * 1e12)
         digest["valu_frac_vop3_rate"] = digest["valu_frac"] * VALU_PEAK_TOPS / VOP3_RATE_TOPS
+        dcyc, _ = issue_cycles(digest["kernel"])
+        if dcyc:
+            digest["valu_frac_issue"] = digest["valu_frac"] * dcyc / 2
         digest["pmc_source"] = dpc["source"]
     if rank == 0:
         line = {

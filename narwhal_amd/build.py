@@ -2,6 +2,7 @@
 
     python -m narwhal_amd.build            # incremental
     python -m narwhal_amd.build --force
+    python narwhal_amd/build.py --hipcc-args OUT   # the argument list (rust/crypto_nwc/build.rs)
 """
 from __future__ import annotations
 
@@ -55,11 +56,17 @@ def up_to_date() -> bool:
     return os.path.exists(OUT) and embedded_id(OUT) == source_id()
 
 
+def hipcc_args(out: str) -> list:
+    """The whole hipcc argument list of libnwc.so (flags, the build id, output, source): the one
+    recipe both this script and the Rust shim's build.rs (`build.py --hipcc-args OUT`) compile
+    with, so a cargo-built library carries the same nwc_build_id as an in-tree one."""
+    return FLAGS + ['-DNWC_BUILD_ID="%s"' % source_id(), "-o", out, os.path.join(CSRC, "nwc_api.hip")]
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return OUT
-    cmd = ([HIPCC] + FLAGS + ['-DNWC_BUILD_ID="%s"' % source_id()] +
-           ["-o", OUT + ".tmp", os.path.join(CSRC, "nwc_api.hip")])
+    cmd = [HIPCC] + hipcc_args(OUT + ".tmp")
     if verbose:
         print("[narwhal_amd.build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -68,4 +75,10 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--hipcc-args" in sys.argv:
+        # rust/crypto_nwc/build.rs: one argument per line
+        print("\n".join(hipcc_args(sys.argv[sys.argv.index("--hipcc-args") + 1])))
+    elif "--source-id" in sys.argv:
+        print(source_id())
+    else:
+        build(force="--force" in sys.argv)

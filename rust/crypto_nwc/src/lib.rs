@@ -42,6 +42,13 @@ pub fn init(device_mask: u32) {
     });
 }
 
+/// The hash of the sources and flags the linked libnwc.so was compiled from (nwc_build_id):
+/// build.rs compiles with the repository's recipe (narwhal_amd/build.py --hipcc-args), so this
+/// equals `python3 narwhal_amd/build.py --source-id` of the same tree; "unknown" for other builds.
+pub fn build_id() -> String {
+    unsafe { CStr::from_ptr(ffi::nwc_build_id()) }.to_string_lossy().into_owned()
+}
+
 fn check(rc: c_int) -> bool {
     if rc < 0 {
         let msg = unsafe { CStr::from_ptr(ffi::nwc_last_error()) };

@@ -59,6 +59,26 @@ def test_every_header_function_is_declared_identically():
         assert r[name] == sig, (name, sig, r[name])
 
 
+def test_build_rs_compiles_with_the_shared_recipe_and_id():
+    """build.rs takes hipcc's whole argument list from narwhal_amd/build.py --hipcc-args (one
+    recipe), whose list carries -DNWC_BUILD_ID=<source_id>: a cargo-built library reports the same
+    build id as the in-tree one (crypto_nwc::build_id), so the provenance check reaches Rust."""
+    import subprocess
+    import sys
+    from narwhal_amd import build as nb
+    rs = open(os.path.join(ROOT, "rust", "crypto_nwc", "build.rs")).read()
+    assert 'arg(src.join("narwhal_amd/build.py"))' in rs and '.arg("--hipcc-args")' in rs
+    assert "Command::new(&hipcc).args(&args)" in rs and "-DNWC_BUILD_ID=" in rs
+    lib = open(os.path.join(ROOT, "rust", "crypto_nwc", "src", "lib.rs")).read()
+    assert "pub fn build_id() -> String" in lib and "nwc_build_id()" in lib
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "narwhal_amd", "build.py"), "--hipcc-args", "/x/libnwc.so"],
+                         capture_output=True, text=True, check=True).stdout.splitlines()
+    assert out == nb.hipcc_args("/x/libnwc.so")
+    assert '-DNWC_BUILD_ID="%s"' % nb.source_id() in out
+    # the in-tree build compiles with exactly this list (build.py: [HIPCC] + hipcc_args(...))
+    assert "[HIPCC] + hipcc_args(" in open(os.path.join(ROOT, "narwhal_amd", "build.py")).read()
+
+
 def test_crate_files_present():
     for f in ("Cargo.toml", "build.rs", "src/lib.rs", "src/ffi.rs"):
         assert os.path.exists(os.path.join(ROOT, "rust", "crypto_nwc", f)), f
