@@ -419,8 +419,13 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
     legs = (("no_cache", False, "leaf", pks, sigs, bad), ("no_cache_straus", False, "straus", pks, sigs, bad),
             ("clean_no_cache", False, "leaf", clean_pks, clean_sigs, no_bad),
             ("clean_no_cache_straus", False, "straus", clean_pks, clean_sigs, no_bad),
+            ("no_cache_msm", False, "msm", pks, sigs, bad),
+            ("clean_no_cache_msm", False, "msm", clean_pks, clean_sigs, no_bad),
             ("launch_keys", False, "launch", pks, sigs, bad), ("cache", True, "leaf", pks, sigs, bad))
+    only = os.environ.get("NWC_BENCH_CFG3_LEGS")   # profiling: a comma-separated subset of the legs
     for tag, use_cache, eq, P, S, want_bad in legs:
+        if only and tag not in only.split(","):
+            continue
         progress("config 3: " + tag)
         _lib.check(lib.nwc_set_committee(None, 0))   # no committee cache, launch keys emptied
         _lib.diag_set("launch_keys", 1 if eq == "launch" else 0)
@@ -431,6 +436,10 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
         if eq == "straus":
             run = lambda: device.cert_reduce(device.verify_batch_straus(cdig, offs, msg_index, P, S, out=words),  # noqa
                                              offs, nv)
+        elif eq == "msm":
+            run = lambda: device.cert_reduce(device.verify_batch_msm(cdig, offs, msg_index, P, S, out=words),  # noqa
+                                             offs, nv)
+            st0 = device.msm_stats()
         else:
             run = lambda: device.cert_reduce(device.verify(cdig, P, S, strict=False, msg_index=msg_index,  # noqa
                                                            out=words), offs, nv)
@@ -450,16 +459,23 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
         out[tag] = {"votes_per_s": nv / dt, "certs_per_s": m / dt, "ms_per_step": dt * 1e3, "parity_ok": ok,
                     "first_call_ms": first_ms,
                     "equation": {"straus": "dalek batch equation over sub-batches of ~12 votes (Straus per lane), leaves for failing sub-batches",
+                                 "msm": "dalek batch equation per group of up to 4,096 votes as a Pippenger MSM (one wave per group, keys "
+                                        "aggregated, wavefront-level bucket reduction), leaves for failing groups",
                                  "launch": "per-vote leaves; the launch's repeated keys detected by the library (no nwc_set_committee), "
                                            "their combs built on the first call, comb kernel from then on"}.get(eq, "per-vote leaves"),
                     "bad_rate": 0.01 if want_bad is bad else 0.0}
+        if eq == "msm":
+            st1 = device.msm_stats()
+            out[tag]["msm_groups"] = {"passed": st1[0] - st0[0], "failed": st1[1] - st0[1],
+                                      "key_overflow": st1[2] - st0[2]}
         if eq == "launch":
             h = ctypes.c_uint32()
             _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
             out[tag]["launch_keys_held"] = h.value
     _lib.check(lib.nwc_set_committee(None, 0))
     _lib.diag_set("launch_keys", 1)
-    out["host_abi_launch_keys"] = bench_cfg3_host_abi(lib, cdig, offs, pks, sigs, bad, m, Q)
+    if not only or "host_abi_launch_keys" in only.split(","):
+        out["host_abi_launch_keys"] = bench_cfg3_host_abi(lib, cdig, offs, pks, sigs, bad, m, Q)
     if cpu_budget > 0:
         out["cpu_baseline"] = cpu_baseline_cfg3(cdig, pks, sigs, m, Q, bad, cpu_budget)
     out["workload"] = "cfg3: %d certificates x %d votes, 1%% invalid, leaf equations + certificate AND + bad-vote set" % (m, Q)

@@ -69,7 +69,8 @@ int nwc_trim(void);
  * once): "straus_nq" = votes per sub-batch of nwc_dev_verify_batch_straus (1..16, default 12,
  * env NWC_STRAUS_NQ); "force_windows" = half-ladder windows forced on every wave (33..37, 0 = off,
  * env NWC_FORCE_WINDOWS; verdicts must not change); "launch_keys" = 0 / 1 (default 1, env
- * NWC_LAUNCH_KEYS; nwc_launch_keys_info).  NWC_ERR_ARG for an unknown name or value.
+ * NWC_LAUNCH_KEYS; nwc_launch_keys_info); "msm_group" = votes per Pippenger group of the MSM
+ * entry (a multiple of 64 in 64..4096; 0, the default = sized per launch; env NWC_MSM_GROUP).  NWC_ERR_ARG for an unknown name or value.
  * Not part of the crate's API. */
 int nwc_diag_set(const char* name, int64_t value);
 
@@ -114,6 +115,18 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
 int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
                                  const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap,
                                  uint8_t* bad_vote_bitmap);
+
+/* The same m certificates through dalek's batch equation as a Pippenger multi-scalar
+ * multiplication over groups of up to 4,096 consecutive votes, one GPU wave per group
+ * (nwc_dev_verify_batch_msm): random 128-bit z_i, the group's distinct keys aggregated (one point
+ * per key), the R points bucketed in LDS with a wavefront-level bucket reduction; the votes of
+ * the groups it rejects are re-decided by the exact per-vote leaves.  Verdicts and bad sets as
+ * nwc_verify_batch_straus_many (deterministic domain exact; dalek's probabilities on its randomized
+ * domain).  A group fails as a whole when any of its votes is bad, so it pays on clean traffic only
+ * (DESIGN.md §4.2e). */
+int nwc_verify_batch_msm_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
+                              const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap,
+                              uint8_t* bad_vote_bitmap);
 
 /* Committee key cache (config/src/lib.rs:154-156 Committee).  Optional: verdicts never
  * depend on it. */
@@ -261,6 +274,19 @@ int nwc_dev_cert_reduce(const void* d_leaf_words, const void* d_offsets, uint64_
 int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, const void* d_msg_index, uint64_t m,
                                 uint64_t nvotes, const void* d_pks, const void* d_sigs, void* d_leaf_words,
                                 void* stream);
+/* Signature::verify_batch over m certificates as dalek's batch equation evaluated by a Pippenger
+ * MSM per group of consecutive votes (up to 4,096, sized so the groups fill whole rounds of the
+ * resident waves; NWC_MSM_GROUP / nwc_diag_set("msm_group") fixes it): one wave per group sorts its
+ * points into 512 buckets per 10-bit
+ * window in LDS and reduces the buckets across its 64 lanes; groups that fail go to the exact
+ * leaves.  Same arguments and leaf-word output as nwc_dev_verify_batch_straus. */
+int nwc_dev_verify_batch_msm(const void* d_digests, const void* d_offsets, const void* d_msg_index, uint64_t m,
+                             uint64_t nvotes, const void* d_pks, const void* d_sigs, void* d_leaf_words,
+                             void* stream);
+/* Groups of the MSM entry on the calling thread's device since nwc_init: passed (their votes'
+ * bits set by the equation), failed (re-decided by the leaves), and of the failed ones, groups with
+ * more distinct keys than the LDS key table holds (128).  Waits for the device.  Diagnostics only. */
+int nwc_msm_stats(uint64_t* groups_passed, uint64_t* groups_failed, uint64_t* key_overflows);
 int nwc_dev_sha512_trunc32(const void* d_data, const void* d_offsets, uint64_t n, void* d_out32,
                            void* stream);
 /* Same, message i = d_data[d_starts[i] .. d_ends[i]) (device u64 arrays): any layout, e.g. a

@@ -42,6 +42,11 @@ _SIGS = {
     "nwc_verify_strict_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p]),
     "nwc_verify_batch_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p, _c_u8p]),
     "nwc_verify_batch_straus_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p, _c_u8p]),
+    "nwc_verify_batch_msm_many": (ctypes.c_int, [_c_u8p, _c_u8p, _c_u8p, _c_u8p, ctypes.c_size_t, _c_u8p, _c_u8p]),
+    "nwc_dev_verify_batch_msm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_void_p]),
+    "nwc_msm_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_set_committee": (ctypes.c_int, [_c_u8p, ctypes.c_size_t]),
     "nwc_cache_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_auto_cache_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

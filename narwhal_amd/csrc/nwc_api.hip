@@ -127,6 +127,9 @@ struct DevCtx {
   int comb_blocks_per_cu = 1;
   uint8_t* straus_scratch = nullptr;   // k_verify_straus per-lane tables (nwc_dev_verify_batch_straus)
   size_t straus_cap = 0;
+  uint8_t* msm_scratch = nullptr;      // k_verify_msm per-wave points and digits (nwc_dev_verify_batch_msm)
+  size_t msm_cap = 0;
+  uint32_t* msm_stats = nullptr;       // groups passed / failed / key overflow (nwc_msm_stats)
   uint32_t* uc_list = nullptr;     // k_verify_comb: equations whose key is not cached
   uint32_t* uc_count = nullptr;
   // k_verify per-lane table slots; reused by every launch, so launches that use it are
@@ -280,10 +283,12 @@ struct Knobs {
   std::atomic<uint32_t> straus_nq{12};
   std::atomic<uint32_t> force_windows{0};
   std::atomic<uint32_t> launch_keys{1};   // NWC_LAUNCH_KEYS: 0 = large batch-leaf launches never build launch keys
+  std::atomic<uint32_t> msm_group{0};     // NWC_MSM_GROUP: votes per Pippenger group of k_verify_msm (0 = sized per launch)
   Knobs() {
     if (const char* e = std::getenv("NWC_LAUNCH_KEYS")) launch_keys = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("NWC_STRAUS_NQ")) straus_nq = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("NWC_FORCE_WINDOWS")) force_windows = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("NWC_MSM_GROUP")) msm_group = (uint32_t)std::strtoul(e, nullptr, 10);
   }
 };
 Knobs& knobs() {
@@ -1243,6 +1248,8 @@ int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8
   if (lanes * stride > d.straus_cap) {
     HIP_TRY(hipStreamSynchronize(s));
     if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
+  if (d.msm_scratch) HIP_TRY(hipFree(d.msm_scratch));
+  d.msm_scratch = nullptr; d.msm_cap = 0;
     d.straus_scratch = nullptr;
     d.straus_cap = 0;
     HIP_TRY(hipMalloc(&d.straus_scratch, lanes * stride));
@@ -1278,6 +1285,82 @@ int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8
   return 0;
 }
 
+
+// dalek's batch equation over groups of consecutive votes as a Pippenger MSM with a wavefront-level
+// bucket reduction (k_verify_msm, msm.h) + the exact leaves for the groups it rejects, on d's
+// stream s: leaf words (a bit per vote) for cert_reduce, like launch_straus.  Caller holds d.mu and
+// has set the device.
+int launch_msm(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8_t* pks, const uint8_t* sigs,
+               uint64_t nvotes, uint64_t* leaf, hipStream_t s) {
+  if (nvotes == 0) return 0;
+  if (nvotes > verify_max_launch()) {
+    const uint64_t step = verify_max_launch();
+    for (uint64_t lo = 0; lo < nvotes; lo += step)
+      if (int rc = launch_msm(d, dig, mi + lo, pks + 32 * lo, sigs + 64 * lo, std::min(step, nvotes - lo), leaf + lo / 64, s))
+        return rc;
+    return 0;
+  }
+  if (!d.comb16)   // no basepoint comb (NWC_COMB16=0): the exact leaves
+    return launch_verify(d, dig, mi, 0, pks, sigs, nvotes, 0, leaf, s);
+  static int bpc = [] {
+    int b = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(nwc::k_verify_msm), 64, 0);
+    return b > 0 ? b : 1;
+  }();
+  const uint64_t slots = (uint64_t)d.cus * bpc;   // resident waves (one group each at a time)
+  uint32_t group = knobs().msm_group.load();
+  if (group == 0) {
+    // as few rounds of the resident waves as groups of <= MSM_GMAX allow, every round full: the
+    // per-window costs of a group (scan, doublings, key points) amortise over larger groups, and a
+    // partial last round would leave waves idle
+    const uint64_t rounds = (nvotes + slots * nwc::MSM_GMAX - 1) / (slots * nwc::MSM_GMAX);
+    group = (uint32_t)((nvotes + slots * rounds - 1) / (slots * rounds));
+  }
+  group = std::min<uint32_t>(nwc::MSM_GMAX, std::max<uint32_t>(64, (group + 63) / 64 * 64));
+  const uint64_t groups = (nvotes + group - 1) / group;
+  const uint64_t grid = std::min<uint64_t>(groups, slots);
+  const size_t need = (size_t)grid * nwc::MSM_WAVE_BYTES;
+  if (need > d.msm_cap) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (d.msm_scratch) HIP_TRY(hipFree(d.msm_scratch));
+    d.msm_scratch = nullptr;
+    d.msm_cap = 0;
+    HIP_TRY(hipMalloc(&d.msm_scratch, need));
+    d.msm_cap = need;
+  }
+  if (!d.msm_stats) {
+    HIP_TRY(hipMalloc(&d.msm_stats, 16));
+    HIP_TRY(hipMemsetAsync(d.msm_stats, 0, 16, s));
+  }
+  // the failing groups' leaves: the list-mode leaf kernel's scratch and lists
+  const uint64_t lgrid = (uint64_t)d.cus * d.verify_blocks_per_cu;
+  if (int rc = ensure_scratch(d, (size_t)lgrid * 256 * 2 * nwc::TAB_BYTES_PER_LANE, nvotes)) return rc;
+  HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
+  nwc::MsmArgs ma{};
+  ma.digests = dig; ma.msg_index = mi; ma.pks = pks; ma.sigs = sigs; ma.nv = nvotes; ma.group = group;
+  {
+    // 32 bytes from the host's CSPRNG per launch (dalek: merlin transcript + thread_rng)
+    static thread_local std::random_device rd;
+    for (int i = 0; i < 8; ++i) ma.seed[i] = rd();
+  }
+  ma.comb16 = d.comb16; ma.scratch = d.msm_scratch;
+  ma.leaf_words = leaf; ma.list = d.uc_list; ma.count = d.uc_count; ma.stats = d.msm_stats;
+  HIP_TRY(hipMemsetAsync(leaf, 0, 8 * ((nvotes + 63) / 64), s));
+  HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
+  hipLaunchKernelGGL(nwc::k_verify_msm, dim3((unsigned)grid), dim3(64), 0, s, ma);
+  HIP_TRY(hipGetLastError());
+  const nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
+                          d.fb_count, 0u, nwc::Committee{}};
+  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
+  hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3((unsigned)lgrid), dim3(256), 0, s, a, ca);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(16), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  if (int rc = launch_torsion(d, pks, leaf, nvotes, d.uc_list, d.uc_count, nwc::Committee{}, s)) return rc;
+  HIP_TRY(hipEventRecord(d.scratch_free, s));
+  return 0;
+}
 
 // Per-vote leaf bits of every device's share (whole certificates) -> certificate verdicts and the
 // bad-vote bitmap (a certificate passes iff every vote's bit is set; an empty one passes).
@@ -1318,7 +1401,7 @@ int batch_verdicts(const uint32_t* offsets, size_t m, const std::vector<uint64_t
 // One device's share of nwc_verify_batch_straus_many: votes [lo, hi) (whole certificates) staged
 // into the arena with one H2D each, the Straus launch, one D2H of the leaf words.
 int straus_range(int di, const uint8_t* digests, size_t m, const uint32_t* offsets, const uint8_t* pks,
-                 const uint8_t* sigs, uint64_t lo, uint64_t hi, std::vector<uint64_t>& out_words) {
+                 const uint8_t* sigs, uint64_t lo, uint64_t hi, std::vector<uint64_t>& out_words, bool msm = false) {
   DevCtx& d = *ctx(di);
   std::lock_guard<std::mutex> lk(d.mu);
   HIP_TRY(hipSetDevice(d.hip_id));
@@ -1345,7 +1428,7 @@ int straus_range(int di, const uint8_t* digests, size_t m, const uint32_t* offse
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(dp, pks + 32 * lo, 32 * n, hipMemcpyHostToDevice, d.stream));
   HIP_TRY(hipMemcpyAsync(ds, sigs + 64 * lo, 64 * n, hipMemcpyHostToDevice, d.stream));
-  if (int rc = launch_straus(d, dm, dmi, dp, ds, n, dout, d.stream)) return rc;
+  if (int rc = (msm ? launch_msm : launch_straus)(d, dm, dmi, dp, ds, n, dout, d.stream)) return rc;
   HIP_TRY(hipMemcpyAsync(out_words.data(), dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
   HIP_TRY(hipStreamSynchronize(d.stream));
   return 0;
@@ -1393,6 +1476,10 @@ int nwc_diag_set(const char* name, int64_t value) {
   if (std::strcmp(name, "straus_nq") == 0) {
     if (value < 1 || value > nwc::STRAUS_MAX_PER_LANE) return set_err(NWC_ERR_ARG, "straus_nq must be in [1, %d]", nwc::STRAUS_MAX_PER_LANE);
     knobs().straus_nq = (uint32_t)value;
+  } else if (std::strcmp(name, "msm_group") == 0) {
+    if (value != 0 && (value < 64 || value > nwc::MSM_GMAX || value % 64))
+      return set_err(NWC_ERR_ARG, "msm_group must be 0 (sized per launch) or a multiple of 64 in [64, %d]", nwc::MSM_GMAX);
+    knobs().msm_group = (uint32_t)value;
   } else if (std::strcmp(name, "launch_keys") == 0) {
     if (value > 1) return set_err(NWC_ERR_ARG, "launch_keys must be 0 or 1");
     knobs().launch_keys = (uint32_t)value;
@@ -1472,6 +1559,8 @@ void nwc_shutdown(void) {
     if (d->comb16_bases) (void)hipFree(d->comb16_bases);
     if (d->kb_bases) (void)hipFree(d->kb_bases);
     if (d->straus_scratch) (void)hipFree(d->straus_scratch);
+    if (d->msm_scratch) (void)hipFree(d->msm_scratch);
+    if (d->msm_stats) (void)hipFree(d->msm_stats);
     if (d->lk_alloc) {
       (void)hipFree(d->lk.keys);
       (void)hipFree(d->lk.flags);
@@ -1594,8 +1683,21 @@ int nwc_verify_batch_many(const uint8_t* digests, const uint32_t* offsets, const
   return r;
 }
 
+static int batch_equation_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks, const uint8_t* sigs,
+                               size_t m, uint8_t* cert_ok_bitmap, uint8_t* bad_vote_bitmap, bool msm);
+
 int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
                                  const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap, uint8_t* bad_vote_bitmap) {
+  return batch_equation_many(digests, offsets, pks, sigs, m, cert_ok_bitmap, bad_vote_bitmap, false);
+}
+
+int nwc_verify_batch_msm_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
+                              const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap, uint8_t* bad_vote_bitmap) {
+  return batch_equation_many(digests, offsets, pks, sigs, m, cert_ok_bitmap, bad_vote_bitmap, true);
+}
+
+static int batch_equation_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks, const uint8_t* sigs,
+                               size_t m, uint8_t* cert_ok_bitmap, uint8_t* bad_vote_bitmap, bool msm) {
   if (int rc = require_init()) return rc;
   if (m == 0) return 0;
   if (!digests || !offsets || !cert_ok_bitmap) return set_err(NWC_ERR_ARG, "null buffer");
@@ -1611,7 +1713,7 @@ int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets
   std::vector<std::vector<uint64_t>> parts(nd);
   std::vector<std::thread> th;
   for (int i = 0; i < nd; ++i)
-    th.emplace_back([&, i] { rc[i] = straus_range(i, digests, m, offsets, pks, sigs, cuts[i], cuts[i + 1], parts[i]); });
+    th.emplace_back([&, i] { rc[i] = straus_range(i, digests, m, offsets, pks, sigs, cuts[i], cuts[i + 1], parts[i], msm); });
   for (auto& t : th) t.join();
   for (int r : rc) if (r < 0) return r;
   return batch_verdicts(offsets, m, cuts, parts, cert_ok_bitmap, bad_vote_bitmap);
@@ -1858,6 +1960,35 @@ int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, co
                        static_cast<uint64_t*>(d_leaf_words), s);
 }
 
+int nwc_dev_verify_batch_msm(const void* d_digests, const void* d_offsets, const void* d_msg_index, uint64_t m,
+                             uint64_t nvotes, const void* d_pks, const void* d_sigs, void* d_leaf_words, void* stream) {
+  DEV_PROLOGUE
+  if (m == 0 || nvotes == 0) return 0;
+  if (!d_digests || !d_offsets || !d_msg_index || !d_pks || !d_sigs || !d_leaf_words)
+    return set_err(NWC_ERR_ARG, "null buffer");
+  return launch_msm(d, static_cast<const uint8_t*>(d_digests), static_cast<const uint32_t*>(d_msg_index),
+                    static_cast<const uint8_t*>(d_pks), static_cast<const uint8_t*>(d_sigs), nvotes,
+                    static_cast<uint64_t*>(d_leaf_words), s);
+}
+
+int nwc_msm_stats(uint64_t* groups_passed, uint64_t* groups_failed, uint64_t* key_overflows) {
+  if (int rc = require_init()) return rc;
+  DevCtx* dp = ctx(t_dev);
+  if (!dp) return set_err(NWC_ERR_ARG, "device index %d not initialised", t_dev);
+  DevCtx& d = *dp;
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.hip_id));
+  uint32_t st[4] = {0, 0, 0, 0};
+  if (d.msm_stats) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(st, d.msm_stats, 16, hipMemcpyDeviceToHost));
+  }
+  if (groups_passed) *groups_passed = st[0];
+  if (groups_failed) *groups_failed = st[1];
+  if (key_overflows) *key_overflows = st[2];
+  return 0;
+}
+
 int nwc_dev_sha512_trunc32(const void* d_data, const void* d_offsets, uint64_t n, void* d_out32, void* stream) {
   DEV_PROLOGUE
   return launch_digest((const uint8_t*)d_data, (const uint64_t*)d_offsets, nullptr, n, (uint8_t*)d_out32, s);
@@ -1963,11 +2094,14 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
 }
 
 // Device part of nwc_sanitize_messages: messages already in HBM (ddata 4-byte aligned with >= 16
-// bytes of readable padding, doff device u64[m+1] rebased so that doff[0] is the first byte).
-// Sizes the arena from `total`; one D2H sync reads the number of vote equations.
-static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total, uint64_t gc_round,
-                 const uint8_t* vote_target, int32_t* dcodes, uint8_t* ddigests, uint32_t* drec, hipStream_t s) {
-  const uint64_t vcap = total / 72 + 1;   // a vote list is allocated only when wholly inside its message (>= 72 B per vote)
+// bytes of readable padding, doff device u64[m+1] relative to ddata).  `total` = the bytes of the
+// whole call (the header-digest scratch is indexed by data offset); `span` = the bytes of these m
+// messages (a chunk of the call), which bound their vote equations.  One D2H sync reads the
+// number of vote equations.
+static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total, uint64_t span,
+                        uint64_t gc_round, const uint8_t* vote_target, int32_t* dcodes, uint8_t* ddigests, uint32_t* drec,
+                        hipStream_t s) {
+  const uint64_t vcap = span / 72 + 1;   // a vote list is allocated only when wholly inside its message (>= 72 B per vote)
   const size_t need = align256(total + 128 * (m + 2)) + align256(32 * m) * 3 + align256(64 * m) +
                       align256(32 * vcap) + align256(64 * vcap) + align256(4 * vcap) + align256(4) +
                       align256(4 * m) + align256(16 * m) + align256(4 * m) +
@@ -2105,7 +2239,8 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
   HIP_TRY(hipMemcpyAsync(doff, hoff.data(), 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
   if (!staged) {
     HIP_TRY(hipMemcpyAsync(ddata, data + base, total, hipMemcpyHostToDevice, d.stream));
-    if (int rc = sanitize_dev(d, ddata, doff, m, total, gc_round, vote_target, dcodes, ddig, drec, d.stream)) return rc;
+    if (int rc = sanitize_dev(d, ddata, doff, m, total, total, gc_round, vote_target, dcodes, ddig, drec, d.stream))
+      return rc;
   } else {
     if (int rc = ensure_stager(d)) return rc;
     while (d.ev_chunk.size() < nch) {
@@ -2117,6 +2252,8 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
     HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
     HIP_TRY(hipStreamWaitEvent(d.xfer, d.ev_fork, 0));
     d.stager->reset();
+    const auto tm0 = std::chrono::steady_clock::now();
+    std::chrono::steady_clock::time_point tm_copied = tm0;
     // a copy thread fills the stages chunk by chunk and records each chunk's event; this thread
     // runs chunk k once its event has been recorded (a wait on an unrecorded event would not wait)
     std::mutex cmu;
@@ -2130,6 +2267,7 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
         e = d.stager->put(ddata + b0, data + base + b0, b1 - b0);
         if (e == hipSuccess) e = d.stager->flush();
         if (e == hipSuccess) e = hipEventRecord(d.ev_chunk[k], d.xfer);
+        if (k + 1 == nch) tm_copied = std::chrono::steady_clock::now();
         std::lock_guard<std::mutex> g(cmu);
         if (e == hipSuccess) recorded = k + 1;
         else copy_err = e;
@@ -2152,13 +2290,21 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
         break;
       }
       const size_t c0 = cuts[k], c1 = cuts[k + 1];
-      rc = sanitize_dev(d, ddata, doff + c0, c1 - c0, total, gc_round, vote_target, dcodes + c0,
+      // the chunk's own byte span bounds its votes (the vote buffers and their clear are per chunk)
+      rc = sanitize_dev(d, ddata, doff + c0, c1 - c0, total, hoff[c1] - hoff[c0], gc_round, vote_target, dcodes + c0,
                         ddig ? ddig + 32 * c0 : nullptr, drec + 4 * c0, d.stream);
     }
     copier.join();
     if (rc) {
       (void)hipStreamSynchronize(d.xfer);   // no copy still writes the arena when the call returns
       return rc;
+    }
+    if (host_timing()) {
+      HIP_TRY(hipStreamSynchronize(d.stream));
+      const auto tm1 = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "nwc sanitize: %zu messages, %.1f MB in %zu chunks: copies queued after %.2f ms, pipeline done %.2f ms later\n",
+                   m, total / 1e6, nch, std::chrono::duration<double>(tm_copied - tm0).count() * 1e3,
+                   std::chrono::duration<double>(tm1 - tm_copied).count() * 1e3);
     }
   }
   HIP_TRY(hipMemcpyAsync(codes, dcodes, 4 * m, hipMemcpyDeviceToHost, d.stream));
@@ -2185,7 +2331,7 @@ int nwc_dev_sanitize_messages(const void* d_data, const void* d_offsets, uint64_
   std::lock_guard<std::mutex> lk(d.mu);
   HIP_TRY(hipSetDevice(d.hip_id));
   if (!d.cc_stakes) return set_err(NWC_ERR_NOT_INIT, "nwc_set_committee_config has not been called");
-  return sanitize_dev(d, static_cast<const uint8_t*>(d_data), static_cast<const uint64_t*>(d_offsets), m, total,
+  return sanitize_dev(d, static_cast<const uint8_t*>(d_data), static_cast<const uint64_t*>(d_offsets), m, total, total,
                       gc_round, vote_target, static_cast<int32_t*>(d_codes), static_cast<uint8_t*>(d_digests32),
                       nullptr, stream ? static_cast<hipStream_t>(stream) : d.stream);
 }
@@ -2216,7 +2362,7 @@ int nwc_memory_info(nwc_memory* out) {
                                                                nwc::KeyComb::windows * sizeof(nwc::ge_p3)) +
                                         4 * (size_t)nwc::LK_SLOTS + 16
                                   : 0);
-    out->scratch = d.scratch_cap + d.straus_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap +
+    out->scratch = d.scratch_cap + d.straus_cap + d.msm_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap +
                    8 * (size_t)d.ts_slot_count;
   }
   out->digesters = digester_device_bytes(d.hip_id);
@@ -2239,6 +2385,8 @@ int nwc_trim(void) {
   HIP_TRY(hipDeviceSynchronize());
   if (d.scratch) HIP_TRY(hipFree(d.scratch));
   if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
+  if (d.msm_scratch) HIP_TRY(hipFree(d.msm_scratch));
+  d.msm_scratch = nullptr; d.msm_cap = 0;
   if (d.arena) HIP_TRY(hipFree(d.arena));
   if (d.msg_arena) HIP_TRY(hipFree(d.msg_arena));
   d.scratch = nullptr; d.scratch_cap = 0;

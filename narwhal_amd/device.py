@@ -76,6 +76,30 @@ def verify_batch_straus(digests: torch.Tensor, offsets: torch.Tensor, msg_index:
     return out
 
 
+def verify_batch_msm(digests: torch.Tensor, offsets: torch.Tensor, msg_index: torch.Tensor, pks: torch.Tensor,
+                     sigs: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dalek's batch equation as a Pippenger MSM per group of consecutive votes (one wave per group,
+    wavefront-level bucket reduction), the exact leaves for the groups it rejects: leaf-style
+    verdict words (bit per vote) for cert_reduce.  Asynchronous."""
+    lib = _lib.load()
+    m = offsets.numel() - 1
+    n = pks.shape[0]
+    assert offsets.dtype == torch.int32 and msg_index.dtype == torch.int32 and msg_index.numel() == n
+    if out is None:
+        out = torch.empty(words_for(n), dtype=torch.int64, device=pks.device)
+    _lib.check(lib.nwc_dev_verify_batch_msm(_ptr(digests), _ptr(offsets), _ptr(msg_index), m, n, _ptr(pks),
+                                            _ptr(sigs), _ptr(out), _stream()))
+    return out
+
+
+def msm_stats():
+    """nwc_msm_stats: (groups passed, groups failed, key overflows) of the MSM entry so far."""
+    lib = _lib.load()
+    v = [ctypes.c_uint64() for _ in range(3)]
+    _lib.check(lib.nwc_msm_stats(*(ctypes.byref(x) for x in v)))
+    return tuple(x.value for x in v)
+
+
 def cert_reduce(leaf_words: torch.Tensor, offsets: torch.Tensor, nvotes: int,
                 want_bad: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     lib = _lib.load()

@@ -44,6 +44,8 @@ extern "C" {
                                  cert_ok_bitmap: *mut u8, bad_vote_bitmap: *mut u8) -> c_int;
     pub fn nwc_verify_batch_straus_many(digests: *const u8, offsets: *const u32, pks: *const u8, sigs: *const u8,
                                         m: usize, cert_ok_bitmap: *mut u8, bad_vote_bitmap: *mut u8) -> c_int;
+    pub fn nwc_verify_batch_msm_many(digests: *const u8, offsets: *const u32, pks: *const u8, sigs: *const u8,
+                                        m: usize, cert_ok_bitmap: *mut u8, bad_vote_bitmap: *mut u8) -> c_int;
     pub fn nwc_set_committee(pks: *const u8, n: usize) -> c_int;
     pub fn nwc_cache_stats(committee_keys: *mut u32, auto_keys: *mut u32) -> c_int;
     pub fn nwc_auto_cache_info(capacity: *mut u32, builds: *mut u64, hits: *mut u64) -> c_int;
@@ -76,6 +78,10 @@ extern "C" {
     pub fn nwc_dev_verify_batch_straus(d_digests: *const c_void, d_offsets: *const c_void, d_msg_index: *const c_void,
                                        m: u64, nvotes: u64, d_pks: *const c_void, d_sigs: *const c_void,
                                        d_leaf_words: *mut c_void, stream: *mut c_void) -> c_int;
+    pub fn nwc_dev_verify_batch_msm(d_digests: *const c_void, d_offsets: *const c_void, d_msg_index: *const c_void,
+                                       m: u64, nvotes: u64, d_pks: *const c_void, d_sigs: *const c_void,
+                                       d_leaf_words: *mut c_void, stream: *mut c_void) -> c_int;
+    pub fn nwc_msm_stats(groups_passed: *mut u64, groups_failed: *mut u64, key_overflows: *mut u64) -> c_int;
     pub fn nwc_dev_sha512_trunc32(d_data: *const c_void, d_offsets: *const c_void, n: u64, d_out32: *mut c_void,
                                   stream: *mut c_void) -> c_int;
     pub fn nwc_dev_sha512_trunc32_ranges(d_data: *const c_void, d_starts: *const c_void, d_ends: *const c_void, n: u64,
