@@ -70,7 +70,9 @@ int nwc_trim(void);
  * env NWC_STRAUS_NQ); "force_windows" = half-ladder windows forced on every wave (33..37, 0 = off,
  * env NWC_FORCE_WINDOWS; verdicts must not change); "launch_keys" = 0 / 1 (default 1, env
  * NWC_LAUNCH_KEYS; nwc_launch_keys_info); "msm_group" = votes per Pippenger group of the MSM
- * entry (a multiple of 64 in 64..4096; 0, the default = sized per launch; env NWC_MSM_GROUP).  NWC_ERR_ARG for an unknown name or value.
+ * entry (a multiple of 64 in 64..4096; 0, the default = sized per launch; env NWC_MSM_GROUP);
+ * "msm_adapt" = 0 / 1 (default 1, env NWC_MSM_ADAPT): the MSM entry's skip policy (0 = the
+ * equation on every group).  NWC_ERR_ARG for an unknown name or value.
  * Not part of the crate's API. */
 int nwc_diag_set(const char* name, int64_t value);
 
@@ -278,15 +280,23 @@ int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, co
  * MSM per group of consecutive votes (up to 4,096, sized so the groups fill whole rounds of the
  * resident waves; NWC_MSM_GROUP / nwc_diag_set("msm_group") fixes it): one wave per group sorts its
  * points into 512 buckets per 10-bit
- * window in LDS and reduces the buckets across its 64 lanes; groups that fail go to the exact
- * leaves.  Same arguments and leaf-word output as nwc_dev_verify_batch_straus. */
+ * window in LDS and reduces the buckets across its 64 lanes.  The votes of groups that fail go
+ * through Straus sub-batches of ~12 (as nwc_dev_verify_batch_straus, fresh z_i), and those of
+ * sub-batches that fail to the exact leaves.  Skip policy (device-side, no host synchronisation):
+ * when more than half of a launch's groups fail (a bad-vote rate of about one per group or more),
+ * the next 7 launches skip the equation and hand every vote straight to the sub-batches; the one
+ * after them runs it on every group again and decides anew.  Same
+ * arguments, leaf-word output and semantics as nwc_dev_verify_batch_straus (on dalek's randomized
+ * domain a vote passes if its group or its sub-batch does: at most ~2/ord). */
 int nwc_dev_verify_batch_msm(const void* d_digests, const void* d_offsets, const void* d_msg_index, uint64_t m,
                              uint64_t nvotes, const void* d_pks, const void* d_sigs, void* d_leaf_words,
                              void* stream);
 /* Groups of the MSM entry on the calling thread's device since nwc_init: passed (their votes'
- * bits set by the equation), failed (re-decided by the leaves), and of the failed ones, groups with
- * more distinct keys than the LDS key table holds (128).  Waits for the device.  Diagnostics only. */
-int nwc_msm_stats(uint64_t* groups_passed, uint64_t* groups_failed, uint64_t* key_overflows);
+ * bits set by the equation), failed (re-decided by the sub-batches), of the failed ones, groups with
+ * more distinct keys than the LDS key table holds (126), and groups the skip policy handed to the
+ * sub-batches without the equation.  Any pointer may be null.  Waits for the device.  Diagnostics
+ * only. */
+int nwc_msm_stats(uint64_t* groups_passed, uint64_t* groups_failed, uint64_t* key_overflows, uint64_t* groups_skipped);
 int nwc_dev_sha512_trunc32(const void* d_data, const void* d_offsets, uint64_t n, void* d_out32,
                            void* stream);
 /* Same, message i = d_data[d_starts[i] .. d_ends[i]) (device u64 arrays): any layout, e.g. a

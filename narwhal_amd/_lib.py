@@ -46,7 +46,7 @@ _SIGS = {
     "nwc_dev_verify_batch_msm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_void_p]),
-    "nwc_msm_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "nwc_msm_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_set_committee": (ctypes.c_int, [_c_u8p, ctypes.c_size_t]),
     "nwc_cache_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "nwc_auto_cache_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

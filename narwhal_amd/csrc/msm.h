@@ -41,7 +41,7 @@ constexpr int MSM_RWIN = 13;                    // windows of z < 2^128 (130 bit
 constexpr int MSM_WIN = 14;                     // windows of the group (a key's sum split at 2^130: < 2^135 each)
 constexpr int MSM_KSPLIT = 130;                 // key point j: sum mod 2^130 on A_j, sum >> 130 on 2^130 A_j
 constexpr int MSM_GMAX = 4096;                  // votes per group (at most)
-constexpr int MSM_KMAX = 128;                   // distinct keys per group (at most)
+constexpr int MSM_KMAX = 126;                   // distinct keys per group (at most; 126 keeps MsmLds in 1/8 of the LDS)
 constexpr int MSM_SLOTS = 256;                  // LDS hash slots of the keys
 constexpr u32 MSM_EMPTY = 0xFFFFFFFFu, MSM_CLAIMED = 0xFFFFFFFEu, MSM_FULL = 0xFFFFFFFDu;
 constexpr int MSM_NPTS = MSM_GMAX + 2 * MSM_KMAX;   // R points, then A_j, then 2^130 A_j
@@ -61,8 +61,27 @@ struct MsmArgs {
   uint64_t* leaf_words;       // bit v = vote v's group passed (zeroed by the caller)
   uint32_t* list;             // votes of the groups that failed (for the exact leaves)
   uint32_t* count;
-  uint32_t* stats;            // [0] groups passed, [1] groups failed, [2] of them: key overflow
+  uint32_t* stats;            // MSM_ST_* words (nwc_msm_stats, the skip policy)
 };
+
+// device-resident MSM statistics and the skip policy's state (u32 words of DevCtx::msm_stats)
+enum : int {
+  MSM_ST_PASSED = 0,    // groups that passed the equation (cumulative)
+  MSM_ST_FAILED = 1,    // groups that failed it (cumulative; a key overflow counts as failed)
+  MSM_ST_OVERFLOW = 2,  // of them: more than MSM_KMAX distinct keys
+  MSM_ST_MODE = 3,      // 0: the equation on every group; k = 1 .. MSM_SKIP_LAUNCHES - 1: on none (k-th such launch)
+  MSM_ST_RUN = 4,       // this launch: groups the equation ran on
+  MSM_ST_RUN_FAILED = 5,// this launch: of them, failed
+  MSM_ST_SKIPPED = 6,   // groups handed to the Straus sub-batches without the equation (cumulative)
+  MSM_ST_WORDS = 8
+};
+// When more than half of a launch's groups fail (a bad-vote rate of ~1/group or more: every group
+// holds one), the next MSM_SKIP_LAUNCHES - 1 launches skip the equation and pass every vote
+// straight to the Straus sub-batches (which a failing group's votes reach anyway, after a wasted
+// MSM); the launch after them runs it on every group again to re-measure.  Skipping within a
+// launch would not help: a wave's group is latency-bound (one group alone takes as long as a full
+// launch, profiles/r05/msm.md), so any probe costs a whole MSM launch -- 1 in 8 amortises it.
+constexpr u32 MSM_SKIP_LAUNCHES = 8;
 
 struct MsmLds {
   union {
@@ -80,6 +99,9 @@ struct MsmLds {
   };
   int16_t kdig[2 * MSM_KMAX][MSM_WIN];   // the key points' digits (phase 1 end -> phase 2): A_j, then 2^130 A_j
 };
+// 8 waves per CU (2 per SIMD, the VGPR limit): a wave's group is latency-bound, so a CU holding 7
+// (128 keys: 20,488 B) ran 1,775 larger groups in the time 2,048 smaller ones take
+static_assert(sizeof(MsmLds) <= 160 * 1024 / 8, "MsmLds must leave room for 8 waves per CU");
 
 // signed radix-2^10 digits (d in [-512, 511]) of a NWORDS-word number; the top window's value is
 // small enough here (z < 2^128 in 13 windows, each half of a key sum < 2^135 in 14) that no carry
@@ -193,9 +215,21 @@ __global__ __launch_bounds__(64, 2) void k_verify_msm(MsmArgs a) {
   int16_t* const rdig = reinterpret_cast<int16_t*>(wbase + (size_t)MSM_NPTS * MSM_POINT_U4 * 16);
   const uint64_t G = a.group;
   const uint64_t ngroups = (a.nv + G - 1) / G;
+  const bool skip = a.stats && a.stats[MSM_ST_MODE] != 0;
   for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const uint64_t v0 = g * G;
     const u32 ng = (u32)(a.nv - v0 < G ? a.nv - v0 : G);
+    if (skip) {
+      // skipped by the policy: the group's votes go to the Straus sub-batches as they are
+      u32 at = 0;
+      if (lane == 0) {
+        at = atomicAdd(a.count, ng);
+        atomicAdd(a.stats + MSM_ST_SKIPPED, 1u);
+      }
+      at = (u32)__shfl((int)at, 0, 64);
+      for (u32 t = lane; t < ng; t += 64) a.list[at + t] = (uint32_t)(v0 + t);
+      continue;
+    }
     // ---------------- phase 1: scalars, R points, key aggregation
     for (u32 i = lane; i < (u32)MSM_SLOTS; i += 64) L.p1.slots[i] = MSM_EMPTY;
     for (u32 i = lane; i < (u32)MSM_KMAX * 8; i += 64) (&L.p1.acc[0][0])[i] = 0ull;
@@ -436,11 +470,31 @@ __global__ __launch_bounds__(64, 2) void k_verify_msm(MsmArgs a) {
       for (u32 t = lane; t < ng; t += 64) a.list[at + t] = (uint32_t)(v0 + t);
     }
     if (lane == 0 && a.stats) {
-      atomicAdd(a.stats + (pass ? 0 : 1), 1u);
-      if (full) atomicAdd(a.stats + 2, 1u);
+      atomicAdd(a.stats + (pass ? MSM_ST_PASSED : MSM_ST_FAILED), 1u);
+      atomicAdd(a.stats + MSM_ST_RUN, 1u);
+      if (!pass) atomicAdd(a.stats + MSM_ST_RUN_FAILED, 1u);
+      if (full) atomicAdd(a.stats + MSM_ST_OVERFLOW, 1u);
     }
     __syncthreads();   // LDS of this group dead before the next group's phase 1
   }
+}
+
+// After each MSM launch (one thread): the next launch's mode (adapt = 0: the equation on every
+// group).
+__global__ void k_msm_policy(uint32_t* st, uint32_t adapt) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const u32 run = st[MSM_ST_RUN], failed = st[MSM_ST_RUN_FAILED];
+  u32 mode = st[MSM_ST_MODE];
+  if (!adapt) {
+    mode = 0;
+  } else if (mode != 0) {
+    mode = mode + 1 < MSM_SKIP_LAUNCHES ? mode + 1 : 0;   // after the skipping launches, re-measure
+  } else if (2 * failed > run) {
+    mode = 1;
+  }
+  st[MSM_ST_MODE] = mode;
+  st[MSM_ST_RUN] = 0;
+  st[MSM_ST_RUN_FAILED] = 0;
 }
 
 }  // namespace nwc

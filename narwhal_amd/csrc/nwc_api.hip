@@ -284,11 +284,13 @@ struct Knobs {
   std::atomic<uint32_t> force_windows{0};
   std::atomic<uint32_t> launch_keys{1};   // NWC_LAUNCH_KEYS: 0 = large batch-leaf launches never build launch keys
   std::atomic<uint32_t> msm_group{0};     // NWC_MSM_GROUP: votes per Pippenger group of k_verify_msm (0 = sized per launch)
+  std::atomic<uint32_t> msm_adapt{1};     // NWC_MSM_ADAPT: 0 = the equation on every group (no skip policy)
   Knobs() {
     if (const char* e = std::getenv("NWC_LAUNCH_KEYS")) launch_keys = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("NWC_STRAUS_NQ")) straus_nq = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("NWC_FORCE_WINDOWS")) force_windows = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("NWC_MSM_GROUP")) msm_group = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("NWC_MSM_ADAPT")) msm_adapt = std::atoi(e) != 0;
   }
 };
 Knobs& knobs() {
@@ -1221,6 +1223,17 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
   return 0;
 }
 
+int ensure_straus_scratch(DevCtx& d, size_t bytes, hipStream_t s) {
+  if (bytes <= d.straus_cap) return 0;
+  HIP_TRY(hipStreamSynchronize(s));
+  if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
+  d.straus_scratch = nullptr;
+  d.straus_cap = 0;
+  HIP_TRY(hipMalloc(&d.straus_scratch, bytes));
+  d.straus_cap = bytes;
+  return 0;
+}
+
 // dalek's batch equation over sub-batches (k_verify_straus) + the exact leaves for the failing
 // sub-batches, on d's stream s: leaf words (a bit per vote) for cert_reduce.  Caller holds d.mu
 // and has set the device.
@@ -1245,16 +1258,7 @@ int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8
   const uint64_t lanes = std::min<uint64_t>((runs + 255) / 256 * 256, resident);
   const uint64_t maxq = (nvotes + runs - 1) / runs;
   const uint64_t stride = maxq * nwc::STRAUS_VOTE_BYTES;
-  if (lanes * stride > d.straus_cap) {
-    HIP_TRY(hipStreamSynchronize(s));
-    if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
-  if (d.msm_scratch) HIP_TRY(hipFree(d.msm_scratch));
-  d.msm_scratch = nullptr; d.msm_cap = 0;
-    d.straus_scratch = nullptr;
-    d.straus_cap = 0;
-    HIP_TRY(hipMalloc(&d.straus_scratch, lanes * stride));
-    d.straus_cap = lanes * stride;
-  }
+  if (int rc = ensure_straus_scratch(d, lanes * stride, s)) return rc;
   // the failing sub-batches' leaves: the list-mode leaf kernel's scratch and lists
   const uint64_t lgrid = (uint64_t)d.cus * d.verify_blocks_per_cu;
   if (int rc = ensure_scratch(d, (size_t)lgrid * 256 * 2 * nwc::TAB_BYTES_PER_LANE, nvotes)) return rc;
@@ -1271,7 +1275,7 @@ int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8
   HIP_TRY(hipMemsetAsync(leaf, 0, 8 * ((nvotes + 63) / 64), s));
   HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
-  hipLaunchKernelGGL(nwc::k_verify_straus, dim3((unsigned)(lanes / 256)), dim3(256), 0, s, sa);
+  hipLaunchKernelGGL(nwc::k_verify_straus<false>, dim3((unsigned)(lanes / 256)), dim3(256), 0, s, sa);
   HIP_TRY(hipGetLastError());
   nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
                     d.fb_count, 0u, nwc::Committee{}};
@@ -1319,7 +1323,9 @@ int launch_msm(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8_t*
   group = std::min<uint32_t>(nwc::MSM_GMAX, std::max<uint32_t>(64, (group + 63) / 64 * 64));
   const uint64_t groups = (nvotes + group - 1) / group;
   const uint64_t grid = std::min<uint64_t>(groups, slots);
-  const size_t need = (size_t)grid * nwc::MSM_WAVE_BYTES;
+  // per-wave points and digits, then the failing groups' vote list (count word, entries)
+  const size_t list_off = align256((size_t)grid * nwc::MSM_WAVE_BYTES);
+  const size_t need = list_off + 256 + 4 * nvotes;
   if (need > d.msm_cap) {
     HIP_TRY(hipStreamSynchronize(s));
     if (d.msm_scratch) HIP_TRY(hipFree(d.msm_scratch));
@@ -1329,10 +1335,19 @@ int launch_msm(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8_t*
     d.msm_cap = need;
   }
   if (!d.msm_stats) {
-    HIP_TRY(hipMalloc(&d.msm_stats, 16));
-    HIP_TRY(hipMemsetAsync(d.msm_stats, 0, 16, s));
+    HIP_TRY(hipMalloc(&d.msm_stats, 4 * nwc::MSM_ST_WORDS));
+    HIP_TRY(hipMemsetAsync(d.msm_stats, 0, 4 * nwc::MSM_ST_WORDS, s));
   }
-  // the failing groups' leaves: the list-mode leaf kernel's scratch and lists
+  uint32_t* const mcount = reinterpret_cast<uint32_t*>(d.msm_scratch + list_off);
+  uint32_t* const mlist = mcount + 64;
+  // the failing groups' votes: Straus sub-batches over the list (runs cut on the device), then the
+  // leaves for the sub-batches that fail -- a group with one bad vote costs ~12 leaf equations, not
+  // one per vote of the group
+  const uint32_t target = std::max<uint32_t>(1, std::min<uint32_t>(knobs().straus_nq.load(), nwc::STRAUS_MAX_PER_LANE));
+  const uint64_t sresident = (uint64_t)d.cus * nwc::STRAUS_WAVES_PER_SIMD * 256;
+  const uint64_t slanes = std::min<uint64_t>(((nvotes + target - 1) / target + 255) / 256 * 256, sresident);
+  const uint64_t sstride = (uint64_t)nwc::STRAUS_MAX_PER_LANE * nwc::STRAUS_VOTE_BYTES;   // runs cut on the device
+  if (int rc = ensure_straus_scratch(d, slanes * sstride, s)) return rc;
   const uint64_t lgrid = (uint64_t)d.cus * d.verify_blocks_per_cu;
   if (int rc = ensure_scratch(d, (size_t)lgrid * 256 * 2 * nwc::TAB_BYTES_PER_LANE, nvotes)) return rc;
   HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
@@ -1344,11 +1359,22 @@ int launch_msm(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8_t*
     for (int i = 0; i < 8; ++i) ma.seed[i] = rd();
   }
   ma.comb16 = d.comb16; ma.scratch = d.msm_scratch;
-  ma.leaf_words = leaf; ma.list = d.uc_list; ma.count = d.uc_count; ma.stats = d.msm_stats;
+  ma.leaf_words = leaf; ma.list = mlist; ma.count = mcount; ma.stats = d.msm_stats;
   HIP_TRY(hipMemsetAsync(leaf, 0, 8 * ((nvotes + 63) / 64), s));
+  HIP_TRY(hipMemsetAsync(mcount, 0, sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(nwc::k_verify_msm, dim3((unsigned)grid), dim3(64), 0, s, ma);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_msm_policy, dim3(1), dim3(64), 0, s, d.msm_stats, (uint32_t)knobs().msm_adapt.load());
+  HIP_TRY(hipGetLastError());
+  nwc::StrausArgs sa{};
+  sa.digests = dig; sa.msg_index = mi; sa.pks = pks; sa.sigs = sigs;
+  for (int i = 0; i < 8; ++i) sa.seed[i] = ma.seed[i] ^ 0x5a5a5a5au;   // fresh z for the second equation
+  sa.comb16 = d.comb16; sa.scratch = d.straus_scratch; sa.lane_stride = sstride;
+  sa.leaf_words = leaf; sa.list = d.uc_list; sa.count = d.uc_count;
+  sa.in_list = mlist; sa.in_count = mcount; sa.target = target;
+  hipLaunchKernelGGL(nwc::k_verify_straus<true>, dim3((unsigned)(slanes / 256)), dim3(256), 0, s, sa);
   HIP_TRY(hipGetLastError());
   const nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
                           d.fb_count, 0u, nwc::Committee{}};
@@ -1480,6 +1506,9 @@ int nwc_diag_set(const char* name, int64_t value) {
     if (value != 0 && (value < 64 || value > nwc::MSM_GMAX || value % 64))
       return set_err(NWC_ERR_ARG, "msm_group must be 0 (sized per launch) or a multiple of 64 in [64, %d]", nwc::MSM_GMAX);
     knobs().msm_group = (uint32_t)value;
+  } else if (std::strcmp(name, "msm_adapt") == 0) {
+    if (value > 1) return set_err(NWC_ERR_ARG, "msm_adapt must be 0 or 1");
+    knobs().msm_adapt = (uint32_t)value;
   } else if (std::strcmp(name, "launch_keys") == 0) {
     if (value > 1) return set_err(NWC_ERR_ARG, "launch_keys must be 0 or 1");
     knobs().launch_keys = (uint32_t)value;
@@ -1971,21 +2000,22 @@ int nwc_dev_verify_batch_msm(const void* d_digests, const void* d_offsets, const
                     static_cast<uint64_t*>(d_leaf_words), s);
 }
 
-int nwc_msm_stats(uint64_t* groups_passed, uint64_t* groups_failed, uint64_t* key_overflows) {
+int nwc_msm_stats(uint64_t* groups_passed, uint64_t* groups_failed, uint64_t* key_overflows, uint64_t* groups_skipped) {
   if (int rc = require_init()) return rc;
   DevCtx* dp = ctx(t_dev);
   if (!dp) return set_err(NWC_ERR_ARG, "device index %d not initialised", t_dev);
   DevCtx& d = *dp;
   std::lock_guard<std::mutex> lk(d.mu);
   HIP_TRY(hipSetDevice(d.hip_id));
-  uint32_t st[4] = {0, 0, 0, 0};
+  uint32_t st[nwc::MSM_ST_WORDS] = {};
   if (d.msm_stats) {
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(st, d.msm_stats, 16, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(st, d.msm_stats, sizeof st, hipMemcpyDeviceToHost));
   }
-  if (groups_passed) *groups_passed = st[0];
-  if (groups_failed) *groups_failed = st[1];
-  if (key_overflows) *key_overflows = st[2];
+  if (groups_passed) *groups_passed = st[nwc::MSM_ST_PASSED];
+  if (groups_failed) *groups_failed = st[nwc::MSM_ST_FAILED];
+  if (key_overflows) *key_overflows = st[nwc::MSM_ST_OVERFLOW];
+  if (groups_skipped) *groups_skipped = st[nwc::MSM_ST_SKIPPED];
   return 0;
 }
 

@@ -53,6 +53,12 @@ struct StrausArgs {
   uint64_t* leaf_words;       // bit v = vote v's sub-batch passed (zeroed by the caller)
   uint32_t* list;             // votes of the sub-batches that failed (for the exact leaves)
   uint32_t* count;
+  // list mode (k_verify_straus<true>): the launch's votes are in_list[0 .. *in_count) (the votes of
+  // the Pippenger groups that failed, msm.h), cut into runs on the device as straus_runs does;
+  // lane_stride must then hold STRAUS_MAX_PER_LANE votes
+  const uint32_t* in_list;
+  const uint32_t* in_count;
+  uint32_t target;
 };
 
 // 128-bit z of global vote index v
@@ -110,11 +116,29 @@ __device__ __forceinline__ i32 nib_digit(const u32* words, int w) {
   return (i32)((words[w >> 3] >> (4 * (w & 7))) & 15u) - 8;
 }
 
+// Sub-batches of a launch of nv votes: each lane slot takes the same number of rounds, and the
+// runs are as close to `target` votes as that allows (never more than STRAUS_MAX_PER_LANE).  A
+// run costs ~253 doublings whatever it holds, so longer runs amortise them; a run with a bad vote
+// is verified again vote by vote, so shorter runs re-verify less at a given bad-vote rate
+// (DESIGN.md §4.2d: target 12 by default, NWC_STRAUS_NQ to A/B).
+__host__ __device__ inline uint64_t straus_runs(uint64_t nv, uint64_t lanes, uint32_t target) {
+  if (target < 1) target = 1;
+  if (target > (uint32_t)STRAUS_MAX_PER_LANE) target = STRAUS_MAX_PER_LANE;
+  const uint64_t want = (nv + target - 1) / target;   // runs of <= target votes
+  if (want <= lanes) return want;
+  // every lane slot runs `rounds` sub-batches, of about `target` votes
+  uint64_t rounds = (want + lanes / 2) / lanes;
+  if (rounds < 1) rounds = 1;
+  while ((nv + rounds * lanes - 1) / (rounds * lanes) > (uint64_t)STRAUS_MAX_PER_LANE) ++rounds;
+  return rounds * lanes;
+}
+
 // The digit words of the current 8 windows, per vote of each lane, staged in LDS every 8 windows
 // (row (2u + k) of 256 words, k = 0 the A digits, 1 the R digits; a wave's access is one 256-B row):
 // the ladder's digit reads then never wait on memory in front of their table gathers.
 constexpr int STRAUS_LDS_WORDS = 2 * STRAUS_MAX_PER_LANE * 256;
 
+template <bool LIST = false>
 __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_straus(StrausArgs a) {
   __shared__ u32 dl[STRAUS_LDS_WORDS];
   const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -127,12 +151,19 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
   // (window, vote) step where it has no vote of its own reads it
   LaneTable{reinterpret_cast<uint4*>(vote_base(0))}.store(0, ge_cached_identity());
   LaneTable{reinterpret_cast<uint4*>(vote_base(0) + TAB_BYTES_PER_LANE)}.store(0, ge_cached_identity());
+  uint64_t nv = a.nv, runs = a.runs;
+  if (LIST) {
+    nv = *a.in_count;
+    runs = straus_runs(nv, lanes, a.target);
+  }
+  // vote of position p: p itself, or in list mode the listed vote
+  auto vote_at = [&](uint64_t p) -> uint64_t { return LIST ? (uint64_t)a.in_list[p] : p; };
   // persistent: lane slot l takes sub-batches l, l + lanes, ...
   for (uint64_t r0 = slot; ; r0 += lanes) {
     // wave-uniform loop exit: every lane of the wave leaves together
-    const bool active = r0 < a.runs;
+    const bool active = r0 < runs;
     if (!__any(active)) break;
-    const uint64_t v0 = active ? r0 * a.nv / a.runs : 0, v1 = active ? (r0 + 1) * a.nv / a.runs : 0;
+    const uint64_t v0 = active ? r0 * nv / runs : 0, v1 = active ? (r0 + 1) * nv / runs : 0;
     const uint32_t nq = (uint32_t)(v1 - v0);
     bool ok = true;
     u32 S[8];
@@ -140,7 +171,7 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
     // ---- phase 1: per vote, decode, scalars, tables
 #pragma unroll 1
     for (uint32_t t = 0; t < nq; ++t) {
-      const uint64_t v = v0 + t;
+      const uint64_t v = vote_at(v0 + t);
       u32 mw[8], aw[8], sg[16];
       load_words8(a.digests + 32 * (uint64_t)a.msg_index[v], mw);
       load_words8(a.pks + 32 * v, aw);
@@ -247,7 +278,12 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
     }
     const bool ident = fe_is_zero(P.X) && fe_is_zero(fe_sub(P.Y, P.Z));
     if (active && nq) {
-      if (ok && ident) {
+      if (ok && ident && LIST) {
+        for (uint64_t p = v0; p < v1; ++p) {
+          const uint64_t v = vote_at(p);
+          atomicOr(reinterpret_cast<unsigned long long*>(a.leaf_words) + (v >> 6), 1ull << (v & 63));
+        }
+      } else if (ok && ident) {
         // the sub-batch's votes pass: set bits v0 .. v1-1 (at most two 64-bit words for nq <= 64)
         for (uint64_t wv = v0 >> 6; wv <= (v1 - 1) >> 6; ++wv) {
           const uint64_t lo = wv << 6;
@@ -258,27 +294,11 @@ __global__ __launch_bounds__(256, NWC_STRAUS_WAVES_PER_SIMD) void k_verify_strau
         }
       } else {
         const uint32_t at = atomicAdd(a.count, nq);
-        for (uint32_t q = 0; q < nq; ++q) a.list[at + q] = (uint32_t)(v0 + q);
+        for (uint32_t q = 0; q < nq; ++q) a.list[at + q] = (uint32_t)vote_at(v0 + q);
       }
     }
   }
 }
 
-// Sub-batches of a launch of nv votes: each lane slot takes the same number of rounds, and the
-// runs are as close to `target` votes as that allows (never more than STRAUS_MAX_PER_LANE).  A
-// run costs ~253 doublings whatever it holds, so longer runs amortise them; a run with a bad vote
-// is verified again vote by vote, so shorter runs re-verify less at a given bad-vote rate
-// (DESIGN.md §4.2d: target 12 by default, NWC_STRAUS_NQ to A/B).
-inline uint64_t straus_runs(uint64_t nv, uint64_t lanes, uint32_t target) {
-  if (target < 1) target = 1;
-  if (target > (uint32_t)STRAUS_MAX_PER_LANE) target = STRAUS_MAX_PER_LANE;
-  const uint64_t want = (nv + target - 1) / target;   // runs of <= target votes
-  if (want <= lanes) return want;
-  // every lane slot runs `rounds` sub-batches, of about `target` votes
-  uint64_t rounds = (want + lanes / 2) / lanes;
-  if (rounds < 1) rounds = 1;
-  while ((nv + rounds * lanes - 1) / (rounds * lanes) > (uint64_t)STRAUS_MAX_PER_LANE) ++rounds;
-  return rounds * lanes;
-}
 
 }  // namespace nwc

@@ -93,9 +93,10 @@ def verify_batch_msm(digests: torch.Tensor, offsets: torch.Tensor, msg_index: to
 
 
 def msm_stats():
-    """nwc_msm_stats: (groups passed, groups failed, key overflows) of the MSM entry so far."""
+    """nwc_msm_stats: (groups passed, groups failed, key overflows, groups skipped) of the MSM entry
+    so far."""
     lib = _lib.load()
-    v = [ctypes.c_uint64() for _ in range(3)]
+    v = [ctypes.c_uint64() for _ in range(4)]
     _lib.check(lib.nwc_msm_stats(*(ctypes.byref(x) for x in v)))
     return tuple(x.value for x in v)
 

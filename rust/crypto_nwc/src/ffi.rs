@@ -81,7 +81,8 @@ extern "C" {
     pub fn nwc_dev_verify_batch_msm(d_digests: *const c_void, d_offsets: *const c_void, d_msg_index: *const c_void,
                                        m: u64, nvotes: u64, d_pks: *const c_void, d_sigs: *const c_void,
                                        d_leaf_words: *mut c_void, stream: *mut c_void) -> c_int;
-    pub fn nwc_msm_stats(groups_passed: *mut u64, groups_failed: *mut u64, key_overflows: *mut u64) -> c_int;
+    pub fn nwc_msm_stats(groups_passed: *mut u64, groups_failed: *mut u64, key_overflows: *mut u64,
+                         groups_skipped: *mut u64) -> c_int;
     pub fn nwc_dev_sha512_trunc32(d_data: *const c_void, d_offsets: *const c_void, n: u64, d_out32: *mut c_void,
                                   stream: *mut c_void) -> c_int;
     pub fn nwc_dev_sha512_trunc32_ranges(d_data: *const c_void, d_starts: *const c_void, d_ends: *const c_void, n: u64,

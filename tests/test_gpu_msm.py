@@ -33,7 +33,17 @@ def _run(digests, offs, pks, sigs):
 
 def _stats():
     from narwhal_amd import device
-    return device.msm_stats()
+    return device.msm_stats()[:3]
+
+
+@pytest.fixture(autouse=True)
+def _every_group():
+    """The exact group counts below need the equation on every group: the skip policy off (a
+    test of its own turns it on)."""
+    from narwhal_amd import _lib
+    _lib.diag_set("msm_adapt", 0)
+    yield
+    _lib.diag_set("msm_adapt", 1)
 
 
 def _committee_certs(oracle, rng, m, q=67, nkeys=100, bad_rate=0.0):
@@ -136,7 +146,7 @@ def test_certificates_vs_oracle(oracle, group):
 
 def test_first_sight_keys_overflow_to_the_leaves(oracle):
     """Votes of distinct keys (first-sight: no repetition to aggregate): a group holds more keys
-    than the LDS table (128) at 2,048 votes a group, so it is decided by the leaves -- verdicts still exact, and
+    than the LDS table (126) at 2,048 votes a group, so it is decided by the leaves -- verdicts still exact, and
     nwc_msm_stats counts the overflow."""
     rng = np.random.default_rng(53)
     m, q = 40, 67
@@ -176,3 +186,37 @@ def test_host_entry_vs_oracle(oracle):
         c = np.unpackbits(np.frombuffer(cert.raw, np.uint8), bitorder="little")[:m].astype(bool)
         b = np.unpackbits(np.frombuffer(badb.raw, np.uint8), bitorder="little")[:nv].astype(bool)
         assert (c == ocert).all() and (b == obad).all(), bad_rate
+
+
+def test_skip_policy_on_a_high_bad_rate(oracle):
+    """A 2 %-bad mix (every group holds bad votes): after the first launch fails its groups, the
+    next 7 skip the equation and pass every vote straight to the Straus sub-batches (nwc_msm_stats:
+    skipped groups), the 8th runs it on every group again; verdicts stay the oracle's throughout,
+    and on clean traffic the equation runs on every group from the next re-measuring launch on."""
+    from narwhal_amd import _lib, device
+    _lib.diag_set("msm_adapt", 1)
+    _lib.diag_set("msm_group", 512)
+    try:
+        rng = np.random.default_rng(59)
+        dig, offs, pks, sigs, _ = _committee_certs(oracle, rng, 400, bad_rate=0.02)
+        ocert, obad = oracle.batch_many(dig, offs.astype(np.uint32), pks, sigs)
+        groups = (int(offs[-1]) + 511) // 512
+        per_call = []
+        for _ in range(9):
+            s0 = device.msm_stats()
+            cert, bad = _run(dig, offs, pks, sigs)
+            s1 = device.msm_stats()
+            assert (cert == ocert).all() and (bad == obad).all()
+            per_call.append((s1[1] - s0[1], s1[3] - s0[3]))   # (failed, skipped)
+        assert per_call == [(groups, 0)] + [(0, groups)] * 7 + [(groups, 0)], per_call
+        cdig, coffs, cpks, csigs, _ = _committee_certs(oracle, rng, 400)
+        per_call = []
+        for _ in range(9):
+            s0 = device.msm_stats()
+            cert, bad = _run(cdig, coffs, cpks, csigs)
+            s1 = device.msm_stats()
+            assert cert.all() and not bad.any()
+            per_call.append((s1[0] - s0[0], s1[3] - s0[3]))   # (passed, skipped)
+        assert per_call == [(0, groups)] * 7 + [(groups, 0)] * 2, per_call
+    finally:
+        _lib.diag_set("msm_group", 0)

@@ -34,7 +34,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {
     "k_verify": "_ZN3nwc8k_verifyILb1ELb0ELb0ELb0EEEvNS_10VerifyArgsENS_8CombArgsE",
     "k_verify_comb": "_ZN3nwc13k_verify_combENS_10VerifyArgsENS_8CombArgsE",
-    "k_verify_straus": "_ZN3nwc15k_verify_strausENS_10StrausArgsE",
+    "k_verify_straus": "_ZN3nwc15k_verify_strausILb0EEEvNS_10StrausArgsE",
     "k_sha512_digest32_sched": "_ZN3nwc23k_sha512_digest32_schedEPKhPKmS3_mPh",
 }
 
