@@ -617,11 +617,11 @@ def bench_cfg3_wire(lib, m: int, steps: int):
     hcodes = np.zeros(m, np.int32)
     flat = buf.reshape(-1)
     hts = []
-    for rep in range(4):   # the first call sizes the staging arena: not timed
+    for rep in range(8):   # the first call sizes the staging arena: not timed
         t0 = time.perf_counter()
         _lib.check(lib.nwc_sanitize_messages(_lib.buf(flat), _lib.buf(hoffs), m, 0, None, _lib.buf(hcodes), None, None))
         hts.append(time.perf_counter() - t0)
-    hdt = sorted(hts[1:])[1]
+    hdt = sorted(hts[1:])[len(hts[1:]) // 2]   # the median of 7 calls (host memory bandwidth varies)
     _lib.check(lib.nwc_set_committee(None, 0))
     return {"workload": "cfg3 wire: %d bincode Certificate messages (100-node committee, 67 parents, 67 votes, "
                         "1%% bad votes) -> DagError codes" % m,

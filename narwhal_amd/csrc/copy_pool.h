@@ -87,6 +87,10 @@ struct HostStager {
   bool used[NST] = {};
   int cur = 0;
   size_t fill = 0;
+  // bytes at which put() flushes the current stage: FIRST after reset(), doubling per flush up
+  // to STAGE, so the first DMA starts after a short fill instead of a whole stage's
+  static constexpr size_t FIRST = 1u << 20;
+  size_t limit = FIRST;
   std::vector<Seg> segs;
   hipStream_t stream = nullptr;
 
@@ -116,13 +120,14 @@ struct HostStager {
   // drop copies queued by a call that failed before its flush (their sources are gone)
   void reset() {
     fill = 0;
+    limit = FIRST;
     segs.clear();
   }
   hipError_t put(uint8_t* dst, const uint8_t* src, size_t len) {
     while (len) {
-      if (fill == STAGE)
+      if (fill >= limit)
         if (hipError_t e = flush()) return e;
-      const size_t take = std::min(len, STAGE - fill);
+      const size_t take = std::min(len, limit - fill);
       segs.push_back(Seg{dst, src, take, fill});
       fill += take;
       dst += take;
@@ -152,6 +157,7 @@ struct HostStager {
     used[cur] = true;
     cur = (cur + 1) % NST;
     fill = 0;
+    limit = std::min(STAGE, 2 * limit);
     segs.clear();
     return hipSuccess;
   }

@@ -85,6 +85,7 @@ struct MsgArgs {
   uint8_t* cdig;                // m x 32: Certificate::digest per message (votes sign it)
   uint32_t* v_total;            // atomic vote-slot allocator
   uint64_t v_cap;
+  uint32_t msg_base;            // the call-wide index of this launch's first message (v_msg entries)
   uint32_t* rec;                // m x 4: kind | flags << 8, post code, vote base, header digest input length
   uint32_t* rec_n;              // m: vote count
   uint32_t* hmatch;             // m: Header::digest == id (k_header_digests)
@@ -577,7 +578,7 @@ __global__ __launch_bounds__(64) void k_parse_messages(MsgArgs a, Committee cm, 
           vr.bytes64(sg);
           st_words(a.v_pk + 32 * (vbase + v), key, 8);
           st_words(a.v_sig + 64 * (vbase + v), sg, 16);
-          a.v_msg[vbase + v] = (uint32_t)i;
+          a.v_msg[vbase + v] = a.msg_base + (uint32_t)i;
           const int kidx = committee_lookup(cm, key);
           weight += member_stake(cc, kidx);
           if (kidx >= 0 && kidx < (int)ncm) atomicMin(&first[kidx], (u32)(v < 0xFFFFFFF0u ? v : 0xFFFFFFF0u));
@@ -694,6 +695,14 @@ __global__ __launch_bounds__(256) void k_header_digests(MsgArgs a) {
 //                UnknownAuthority (first vote) -> CertificateRequiresQuorum -> InvalidSignature
 //                                                            (core.rs:338-346, messages.rs:189-215)
 //   vote:        Serialization -> TooOld -> UnexpectedVote -> UnknownAuthority -> InvalidSignature
+// The shared vote-slot counter of a chunked call rounded up to a multiple of 64 (<= cap).
+__global__ void k_align_slots(uint32_t* v_total, uint32_t cap) {
+  if (threadIdx.x == 0) {
+    const uint32_t v = (*v_total + 63u) & ~63u;
+    *v_total = v < cap ? v : cap;
+  }
+}
+
 __global__ void k_finalize_messages(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ rec_n,
                                     const uint32_t* __restrict__ hmatch, const uint64_t* __restrict__ strict_bits,
                                     const uint64_t* __restrict__ leaf_bits, uint64_t m, int32_t* __restrict__ codes) {

@@ -21,6 +21,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <functional>
 #include <thread>
 #include <unordered_set>
 #include <vector>
@@ -116,6 +117,7 @@ struct DevCtx {
   // `stream` (one event per chunk in flight, created on first use)
   hipStream_t xfer = nullptr;
   std::vector<hipEvent_t> ev_chunk;
+  std::vector<hipEvent_t> ev_cnt;      // sanitize: chunk k's vote count copied to the host
   nwc::ge_niels* base_table = nullptr;
   nwc::ge_niels_pad* base24 = nullptr;   // radix-2^24 basepoint tables (2.1 GB)
   nwc::ge_p3* base24_points = nullptr;    // B and 2^141 B
@@ -234,10 +236,13 @@ struct DevCtx {
 #define NWC_HOST_CHUNK_MAX (1u << 20)
 #endif
 #ifndef NWC_MSG_CHUNK
-#define NWC_MSG_CHUNK (72u << 20)   // bytes of wire messages per pipelined chunk of nwc_sanitize_messages (A/B: profiles/r04/ab_wire_host_chunks.txt)
+#define NWC_MSG_CHUNK (24u << 20)   // largest pipelined chunk of nwc_sanitize_messages, bytes of wire messages (A/B: profiles/r05/wire_host.md)
 #endif
 #ifndef NWC_HOST_CHUNK_GROWTH
 #define NWC_HOST_CHUNK_GROWTH 3
+#endif
+#ifndef NWC_LEAF_ROUNDS
+#define NWC_LEAF_ROUNDS 0   // nwc_sanitize_messages from host memory: leaf launch granularity (A/B: profiles/r05/wire_host.md)
 #endif
 #ifndef NWC_PINNED_STAGE_MAX
 #define NWC_PINNED_STAGE_MAX (1u << 20)
@@ -1625,6 +1630,7 @@ void nwc_shutdown(void) {
     if (d->stager) d->stager->release();
     d->stager.reset();
     for (hipEvent_t e : d->ev_chunk) (void)hipEventDestroy(e);
+    for (hipEvent_t e : d->ev_cnt) (void)hipEventDestroy(e);
     if (d->xfer) (void)hipStreamDestroy(d->xfer);
     if (d->stream) (void)hipStreamDestroy(d->stream);
   }
@@ -2123,19 +2129,27 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
   return 0;
 }
 
-// Device part of nwc_sanitize_messages: messages already in HBM (ddata 4-byte aligned with >= 16
-// bytes of readable padding, doff device u64[m+1] relative to ddata).  `total` = the bytes of the
-// whole call (the header-digest scratch is indexed by data offset); `span` = the bytes of these m
-// messages (a chunk of the call), which bound their vote equations.  One D2H sync reads the
-// number of vote equations.
-static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total, uint64_t span,
-                        uint64_t gc_round, const uint8_t* vote_target, int32_t* dcodes, uint8_t* ddigests, uint32_t* drec,
-                        hipStream_t s) {
-  const uint64_t vcap = span / 72 + 1;   // a vote list is allocated only when wholly inside its message (>= 72 B per vote)
-  const size_t need = align256(total + 128 * (m + 2)) + align256(32 * m) * 3 + align256(64 * m) +
-                      align256(32 * vcap) + align256(64 * vcap) + align256(4 * vcap) + align256(4) +
-                      align256(4 * m) + align256(16 * m) + align256(4 * m) +
-                      align256(8 * ((m + 63) / 64)) + align256(8 * ((vcap + 63) / 64));
+// Device part of nwc_sanitize_messages: messages in HBM (ddata 4-byte aligned with >= 16 bytes
+// of readable padding, doff device u64[m+1] relative to ddata, `total` bytes), parsed as the
+// chunks cuts[k] .. cuts[k+1] (whole messages).  `chunk_ready(k)`, when given, returns once chunk
+// k's bytes are on their way and stream s waits for them (the host path's copies).  The chunks
+// share one vote-slot counter, so the votes of the chunks parsed so far are contiguous; after each
+// parse the host reads the count and launches the leaves of whole rounds of the leaf kernel's
+// resident lanes (a partial round costs a full one's time), on the side stream beside the next
+// chunk's parse, and the rest after the last chunk.  The strict equations (headers' and votes'
+// own signatures) of all chunks but the last run while the last one crosses PCIe; the header
+// digests and the final codes run once over all m messages.
+static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total,
+                        const std::vector<size_t>& cuts, uint64_t gc_round, const uint8_t* vote_target, int32_t* dcodes,
+                        uint8_t* ddigests, uint32_t* drec, hipStream_t s,
+                        const std::function<int(size_t)>& chunk_ready = nullptr) {
+  const size_t nch = cuts.size() - 1;
+  // a vote list is allocated only when wholly inside its message (>= 72 B per vote)
+  const uint64_t vt = total / 72 + 1 + (nch > 1 ? 64 * nch : 0);   // + the 64-slot alignment of each chunk
+  if (vt > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "too many vote slots in one call");
+  const size_t need = align256(total + 128 * (m + 2)) + align256(32 * m) * 3 + align256(64 * m) + align256(32 * vt) +
+                      align256(64 * vt) + align256(4 * vt) + align256(4) + align256(4 * m) + align256(16 * m) +
+                      align256(4 * m) + align256(8 * ((m + 63) / 64)) + align256(8 * ((vt + 63) / 64));
   if (need > d.msg_arena_cap) {
     HIP_TRY(hipEventSynchronize(d.scratch_free));
     HIP_TRY(hipStreamSynchronize(s));
@@ -2147,7 +2161,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     d.msg_arena_cap = cap;
   }
   Carve c(d.msg_arena);
-  nwc::MsgArgs a{};
+  nwc::MsgArgs a{};   // the whole call's arrays
   a.data = ddata;
   a.offsets = doff;
   a.m = m;
@@ -2157,16 +2171,16 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   a.eq_pk = c.take<uint8_t>(32 * m);
   a.eq_sig = c.take<uint8_t>(64 * m);
   a.cdig = c.take<uint8_t>(32 * m);
-  a.v_pk = c.take<uint8_t>(32 * vcap);
-  a.v_sig = c.take<uint8_t>(64 * vcap);
-  a.v_msg = c.take<uint32_t>(4 * vcap);
+  a.v_pk = c.take<uint8_t>(32 * vt);
+  a.v_sig = c.take<uint8_t>(64 * vt);
+  a.v_msg = c.take<uint32_t>(4 * vt);
   a.v_total = c.take<uint32_t>(4);
-  a.v_cap = vcap;
+  a.v_cap = vt;
   a.hmatch = c.take<uint32_t>(4 * m);
   a.rec = drec ? drec : c.take<uint32_t>(16 * m);
   a.rec_n = c.take<uint32_t>(4 * m);
   uint64_t* sbits = c.take<uint64_t>(8 * ((m + 63) / 64));
-  uint64_t* lbits = c.take<uint64_t>(8 * ((vcap + 63) / 64));
+  uint64_t* lbits = c.take<uint64_t>(8 * ((vt + 63) / 64));
   a.digests = ddigests;
   if (vote_target) {
     a.target.enabled = 1;
@@ -2174,37 +2188,136 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     std::memcpy(&a.target.round, vote_target + 32, 8);
     std::memcpy(a.target.origin, vote_target + 40, 32);
   }
+  if (int rc = d.ensure_pinned(NWC_PINNED_STAGE_MAX)) return rc;
+  if (4 * nch > (64u << 10)) return set_err(NWC_ERR_ARG, "too many chunks");   // counts below sanitize_range's offsets
+  uint32_t* nv_host = reinterpret_cast<uint32_t*>(d.pinned);   // pinned: the count copies stay asynchronous
+  while (d.ev_cnt.size() < nch) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    d.ev_cnt.push_back(e);
+  }
+  // the leaf stream when chunks overlap: the side stream, which has a hardware queue of its own
+  // (GPU_MAX_HW_QUEUES = 4: a stream created later shared the transfer stream's queue, and its
+  // leaves waited behind the markers of the in-flight copies, profiles/r05/wire_host.md)
+  // NWC_LEAF_STREAM=0: the leaves on s behind the parses (no overlap of the two, A/B)
+  static const bool leaf_side = [] {
+    const char* e = std::getenv("NWC_LEAF_STREAM");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  const bool chunked = nch > 1;
+  const hipStream_t ls = chunked && leaf_side ? d.side : s;
   HIP_TRY(hipMemsetAsync(a.v_total, 0, 4, s));
-  HIP_TRY(hipMemsetAsync(a.v_msg, 0, 4 * vcap, s));
+  HIP_TRY(hipMemsetAsync(a.v_msg, 0, 4 * vt, s));
   const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
   const nwc::CommitteeCfg cc{d.cc_stakes, d.cc_worker_off, d.cc_worker_ids, d.cc_quorum, d.cc_n};
   const size_t first_lds = 4 * (size_t)std::max<uint32_t>(1, std::min<uint32_t>(d.cc_n, nwc::MSG_MAX_COMMITTEE));
-  hipLaunchKernelGGL(nwc::k_parse_messages, dim3((unsigned)m), dim3(64), first_lds, s, a, cm, cc);
-  HIP_TRY(hipGetLastError());
-  // Header::digest checks on the side stream, beside the signature launches (only the final
-  // kernel reads their result); launch_verify's own side-stream work queues behind them
-  HIP_TRY(hipEventRecord(d.ev_fork, s));
-  HIP_TRY(hipStreamWaitEvent(d.side, d.ev_fork, 0));
-  hipLaunchKernelGGL(nwc::k_header_digests, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.side, a);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(d.ev_msg, d.side));
-  // the vote count sizes the leaf launch: read it behind the parse, and let the strict launch
-  // (headers' and votes' signatures, which does not need it) run while the host waits for it
-  // (into pinned memory: a pageable destination would make the copy synchronous)
-  if (int rc = d.ensure_pinned(NWC_PINNED_STAGE_MAX)) return rc;
-  uint32_t* nv_host = reinterpret_cast<uint32_t*>(d.pinned);
-  HIP_TRY(hipMemcpyAsync(nv_host, a.v_total, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipEventRecord(d.ev_count, s));
-  if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, m, 1, sbits, s)) return rc;
-  HIP_TRY(hipEventSynchronize(d.ev_count));
-  const uint64_t nvotes = std::min<uint64_t>(*nv_host, vcap);
-  // the batch leaves (certificate votes)
-  if (nvotes)
-    if (int rc = launch_verify(d, a.cdig, a.v_msg, 0, a.v_pk, a.v_sig, nvotes, 0, lbits, s)) return rc;
-  HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
+  // NWC_HOST_TIMING: host-side stamps of the steps (which call waits on what)
+  const bool timing = host_timing();
+  const auto tm0 = std::chrono::steady_clock::now();
+  std::vector<std::pair<const char*, double>> marks;
+  auto mark = [&](const char* what) {
+    if (timing) marks.emplace_back(what, std::chrono::duration<double>(std::chrono::steady_clock::now() - tm0).count() * 1e3);
+  };
+  // leaf launches in units of `leaf_rounds` rounds of the leaf kernel's resident lanes (the
+  // committee comb kernel's: one equation per lane a round); 0 = one launch per chunk
+  static const uint64_t leaf_rounds = [] {
+    const char* e = std::getenv("NWC_LEAF_ROUNDS");
+    return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)NWC_LEAF_ROUNDS;
+  }();
+  const uint64_t round = leaf_rounds ? std::max<uint64_t>(64, leaf_rounds * d.cus * d.comb_blocks_per_cu * 256) : 64;
+  uint64_t launched = 0;   // votes [0, launched) have their leaf launch queued
+  auto leaves = [&](uint64_t upto) -> int {
+    if (upto <= launched) return 0;
+    const int rc = launch_verify(d, a.cdig, a.v_msg + launched, 0, a.v_pk + 32 * launched, a.v_sig + 64 * launched,
+                                 upto - launched, 0, lbits + launched / 64, ls);
+    launched = upto;
+    mark("leaves queued");
+    return rc;
+  };
+  uint64_t nv = 0;
+  for (size_t k = 0; k < nch; ++k) {
+    if (chunk_ready)
+      if (int rc = chunk_ready(k)) return rc;
+    mark("chunk ready");
+    const size_t c0 = cuts[k];
+    nwc::MsgArgs ak = a;
+    ak.offsets = doff + c0;
+    ak.m = cuts[k + 1] - c0;
+    ak.hashbuf = a.hashbuf + 128 * c0;   // the message's slot: aligned data offset + 128 x (call-wide index)
+    ak.eq_msg = a.eq_msg + 32 * c0;
+    ak.eq_pk = a.eq_pk + 32 * c0;
+    ak.eq_sig = a.eq_sig + 64 * c0;
+    ak.cdig = a.cdig + 32 * c0;
+    ak.msg_base = (uint32_t)c0;
+    ak.hmatch = a.hmatch + c0;
+    ak.rec = a.rec + 4 * c0;
+    ak.rec_n = a.rec_n + c0;
+    ak.digests = ddigests ? ddigests + 32 * c0 : nullptr;
+    hipLaunchKernelGGL(nwc::k_parse_messages, dim3((unsigned)ak.m), dim3(64), first_lds, s, ak, cm, cc);
+    HIP_TRY(hipGetLastError());
+    if (nch > 1) {
+      // the next chunk's votes from a 64-slot boundary: every leaf launch starts on its own
+      // verdict word (the skipped slots belong to no message; their leaves are never read)
+      hipLaunchKernelGGL(nwc::k_align_slots, dim3(1), dim3(64), 0, s, a.v_total, (uint32_t)vt);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(nv_host + k, a.v_total, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(d.ev_cnt[k], s));
+    mark("parse queued");
+    if (!chunked) continue;
+    // the votes parsed so far, in whole rounds, on the leaf stream; the next chunk's copy goes
+    // on in the copier thread meanwhile, and its parse runs beside these leaves
+    HIP_TRY(hipEventSynchronize(d.ev_cnt[k]));
+    nv = std::min<uint64_t>(nv_host[k], vt);
+    mark("count");
+    if (ls != s) HIP_TRY(hipStreamWaitEvent(ls, d.ev_cnt[k], 0));
+    // (before the last chunk every vote so far: the last leaf launch then holds only the last
+    // chunk's votes)
+    if (k + 2 == nch || (k + 1 < nch && !leaf_rounds))
+      if (int rc = leaves(nv)) return rc;
+    if (k + 2 < nch && leaf_rounds)
+      if (int rc = leaves(launched + (nv - launched) / round * round)) return rc;
+    // the strict equations of every chunk but the last while the last one crosses PCIe
+    // (cuts[nch - 1] is a multiple of 64 messages: the two strict launches own their words)
+    if (k + 2 == nch)
+      if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, cuts[k + 1], 1, sbits, ls)) return rc;
+  }
+  if (chunked) {
+    // the Header::digest checks once, beside the last leaves (latency-bound: ~0.2 ms for any
+    // number of messages, so not per chunk)
+    hipLaunchKernelGGL(nwc::k_header_digests, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a);
+    HIP_TRY(hipGetLastError());
+    const size_t c0 = cuts[nch - 1];
+    if (int rc = launch_verify(d, a.eq_msg + 32 * c0, nullptr, 1, a.eq_pk + 32 * c0, a.eq_sig + 64 * c0, m - c0, 1,
+                               sbits + c0 / 64, ls))
+      return rc;
+    if (int rc = leaves(nv)) return rc;
+    if (ls != s) {
+      HIP_TRY(hipEventRecord(d.ev_msg, ls));
+      HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
+    }
+  } else {
+    // one chunk: the strict launch (it needs no count) queued before the host waits for the
+    // count, the Header::digest checks beside the leaves on the side stream
+    if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, m, 1, sbits, s)) return rc;
+    HIP_TRY(hipEventRecord(d.ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(d.side, d.ev_fork, 0));
+    hipLaunchKernelGGL(nwc::k_header_digests, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.side, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(d.ev_msg, d.side));
+    HIP_TRY(hipEventSynchronize(d.ev_cnt[0]));
+    if (int rc = leaves(std::min<uint64_t>(nv_host[0], vt))) return rc;
+    HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
+  }
   hipLaunchKernelGGL(nwc::k_finalize_messages, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a.rec,
                      a.rec_n, a.hmatch, sbits, lbits, (uint64_t)m, dcodes);
   HIP_TRY(hipGetLastError());
+  mark("final queued");
+  if (timing && nch > 1) {
+    std::string line;
+    for (const auto& mk : marks) line += std::string(" ") + mk.first + "@" + std::to_string(mk.second).substr(0, 5);
+    std::fprintf(stderr, "nwc sanitize steps:%s\n", line.c_str());
+  }
   return 0;
 }
 
@@ -2255,21 +2368,46 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
     const char* e = std::getenv("NWC_MSG_CHUNK");   // 0 = one copy, then one pass (A/B)
     return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)NWC_MSG_CHUNK;
   }();
+  // chunk sizes: from 16 MB doubling up to msg_chunk, and never more than half of what remains
+  // (>= 8 MB, so the last one is <= 16 MB): the first parse starts after a short copy, and the
+  // work left when the last copy lands (that chunk's parse, leaves and strict equations, the
+  // codes) is small; each leaf launch costs >= ~0.18 ms whatever its size, so not smaller
   std::vector<size_t> cuts{0};
-  if (staged && msg_chunk && total >= 2 * msg_chunk) {
-    const uint64_t nch = (total + msg_chunk - 1) / msg_chunk;
-    for (uint64_t k = 1; k < nch; ++k) {
-      const size_t cm = (size_t)(std::lower_bound(hoff.begin(), hoff.end(), total * k / nch) - hoff.begin());
-      if (cm > cuts.back() && cm < m) cuts.push_back(cm);
+  const uint64_t lo = std::min<uint64_t>((uint64_t)8 << 20, msg_chunk);
+  if (staged && msg_chunk && total >= 4 * lo) {
+    uint64_t at = 0, next = 2 * lo;
+    while (total - at > 2 * lo) {
+      const uint64_t want = std::max(lo, std::min(next, (total - at) / 2));
+      const size_t cm = (size_t)(std::lower_bound(hoff.begin(), hoff.end(), at + want) - hoff.begin());
+      if (cm <= cuts.back() || cm >= m) break;
+      cuts.push_back(cm);
+      at = hoff[cm];
+      next = std::min<uint64_t>(msg_chunk, 2 * next);
+    }
+    // the last cut on a multiple of 64 messages (the strict launches' verdict words)
+    while (cuts.size() > 1 && (cuts.back() & 63)) {
+      const size_t c = cuts.back() & ~(size_t)63;
+      cuts.pop_back();
+      if (c > cuts.back()) cuts.push_back(c);
     }
   }
   cuts.push_back(m);
   const size_t nch = cuts.size() - 1;
   HIP_TRY(hipMemsetAsync(ddata + total, 0, 16, d.stream));
-  HIP_TRY(hipMemcpyAsync(doff, hoff.data(), 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
+  // the offsets through pinned memory when they fit beside the chunk counts (a pageable source
+  // makes the copy wait for the host)
+  const size_t hoff_at = 64u << 10;
+  if (8 * (m + 1) <= NWC_PINNED_STAGE_MAX - hoff_at) {
+    if (int rc = d.ensure_pinned(NWC_PINNED_STAGE_MAX)) return rc;
+    uint8_t* const ph = static_cast<uint8_t*>(d.pinned) + hoff_at;
+    std::memcpy(ph, hoff.data(), 8 * (m + 1));
+    HIP_TRY(hipMemcpyAsync(doff, ph, 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
+  } else {
+    HIP_TRY(hipMemcpyAsync(doff, hoff.data(), 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
+  }
   if (!staged) {
     HIP_TRY(hipMemcpyAsync(ddata, data + base, total, hipMemcpyHostToDevice, d.stream));
-    if (int rc = sanitize_dev(d, ddata, doff, m, total, total, gc_round, vote_target, dcodes, ddig, drec, d.stream))
+    if (int rc = sanitize_dev(d, ddata, doff, m, total, {0, m}, gc_round, vote_target, dcodes, ddig, drec, d.stream))
       return rc;
   } else {
     if (int rc = ensure_stager(d)) return rc;
@@ -2304,27 +2442,19 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
         ccv.notify_all();
       }
     });
-    int rc = 0;
-    for (size_t k = 0; k < nch && rc == 0; ++k) {
+    auto chunk_ready = [&](size_t k) -> int {
       {
         std::unique_lock<std::mutex> g(cmu);
         ccv.wait(g, [&] { return recorded > k || copy_err != hipSuccess; });
-        if (recorded <= k) {
-          rc = set_err(NWC_ERR_DEVICE, "message copy: %s", hipGetErrorString(copy_err));
-          break;
-        }
+        if (recorded <= k) return set_err(NWC_ERR_DEVICE, "message copy: %s", hipGetErrorString(copy_err));
       }
       const hipError_t e = hipStreamWaitEvent(d.stream, d.ev_chunk[k], 0);
-      if (e != hipSuccess) {
-        rc = set_err(NWC_ERR_DEVICE, "hipStreamWaitEvent: %s", hipGetErrorString(e));
-        break;
-      }
-      const size_t c0 = cuts[k], c1 = cuts[k + 1];
-      // the chunk's own byte span bounds its votes (the vote buffers and their clear are per chunk)
-      rc = sanitize_dev(d, ddata, doff + c0, c1 - c0, total, hoff[c1] - hoff[c0], gc_round, vote_target, dcodes + c0,
-                        ddig ? ddig + 32 * c0 : nullptr, drec + 4 * c0, d.stream);
-    }
-    copier.join();
+      if (e != hipSuccess) return set_err(NWC_ERR_DEVICE, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+      return 0;
+    };
+    int rc = sanitize_dev(d, ddata, doff, m, total, cuts, gc_round, vote_target, dcodes, ddig, drec, d.stream,
+                          chunk_ready);
+    copier.join();   // the copier never waits on this thread: it runs through every chunk
     if (rc) {
       (void)hipStreamSynchronize(d.xfer);   // no copy still writes the arena when the call returns
       return rc;
@@ -2361,8 +2491,8 @@ int nwc_dev_sanitize_messages(const void* d_data, const void* d_offsets, uint64_
   std::lock_guard<std::mutex> lk(d.mu);
   HIP_TRY(hipSetDevice(d.hip_id));
   if (!d.cc_stakes) return set_err(NWC_ERR_NOT_INIT, "nwc_set_committee_config has not been called");
-  return sanitize_dev(d, static_cast<const uint8_t*>(d_data), static_cast<const uint64_t*>(d_offsets), m, total, total,
-                      gc_round, vote_target, static_cast<int32_t*>(d_codes), static_cast<uint8_t*>(d_digests32),
+  return sanitize_dev(d, static_cast<const uint8_t*>(d_data), static_cast<const uint64_t*>(d_offsets), m, total,
+                      {0, (size_t)m}, gc_round, vote_target, static_cast<int32_t*>(d_codes), static_cast<uint8_t*>(d_digests32),
                       nullptr, stream ? static_cast<hipStream_t>(stream) : d.stream);
 }
 
