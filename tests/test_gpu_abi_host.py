@@ -211,6 +211,19 @@ def test_c_host_under_asan(oracle, golden_verify, golden_batch):
     # the sanitizer is live in this process layout: an out-of-bounds heap read is reported
     r = subprocess.run([ASAN_BIN], input="Z\n", capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "heap-buffer-overflow" in r.stderr, (r.returncode, r.stderr[-500:])
+    # the whole exit path -- main's return: the atexit handlers, libnwc's static destructors, the
+    # HIP/HSA runtime's own teardown -- with ASan's quarantine off.  With it on, ASan recycles a
+    # quarantined device-allocator chunk inside libamdhip64's __cxa_finalize and aborts on its
+    # CHECK "dev_runtime_unloaded_" (no libnwc frame on that stack; 2 of 2 runs abort with the
+    # quarantine, 0 of 3 without: profiles/r05/asan_exit.md)
+    r = subprocess.run([ASAN_BIN], input="\n".join(lines[:len(golden_batch)] + ["Y 4 2"]) + "\n", capture_output=True,
+                       text=True, timeout=300,
+                       env=dict(env, NWC_HOST_EXIT="return", ASAN_OPTIONS=env["ASAN_OPTIONS"] + ":quarantine_size_mb=0"))
+    if r.returncode != 0:
+        _keep_report("abi_host_asan_exit", r)
+    assert r.returncode == 0, (r.returncode, _report_head(r.stderr))
+    assert "AddressSanitizer" not in r.stderr and "CHECK failed" not in r.stderr, r.stderr[-3000:]
+    assert [l.rstrip() for l in r.stdout.splitlines()] == want[:len(golden_batch)] + ["Y 0"], r.stdout[-1000:]
 
 
 def _same(got: str, want) -> bool:

@@ -6,7 +6,7 @@ handlers, libnwc's static destructors and the HIP/HSA runtime's own teardown) in
 Every run's stderr is kept under gpurun_out/asan_exit_<k>.stderr; the summary line per run says
 whether ASan reported, and the frames of the first report are printed.
 
-    python tools/asan_exit_probe.py [runs]
+    python tools/asan_exit_probe.py [runs] [extra ASAN_OPTIONS, e.g. quarantine_size_mb=0]
 """
 import json
 import os
@@ -44,14 +44,19 @@ def requests():
 
 def main():
     runs = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    extra = sys.argv[2] if len(sys.argv) > 2 else ""
     from tests.test_gpu_abi_host import ASAN_BIN, asan_env
     inp = requests()
+    env = asan_env(NWC_HOST_EXIT="return")
+    if extra:
+        env["ASAN_OPTIONS"] += ":" + extra
+    print("ASAN_OPTIONS=" + env["ASAN_OPTIONS"], flush=True)
     out_dir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out_dir, exist_ok=True)
     first = None
     for k in range(runs):
         r = subprocess.run([ASAN_BIN], input=inp, capture_output=True, text=True, timeout=300,
-                           env=asan_env(NWC_HOST_EXIT="return"))
+                           env=env)
         open(os.path.join(out_dir, "asan_exit_%d.stderr" % k), "w").write(r.stderr)
         rep = "==ERROR" in r.stderr or "CHECK failed" in r.stderr or "AddressSanitizer" in r.stderr
         print("run %d: rc %d, sanitizer report: %s, lines out %d" % (k, r.returncode, rep, len(r.stdout.splitlines())),
