@@ -61,7 +61,7 @@ CFG4_BATCH_BYTES = 12 + CFG4_TXS * (8 + CFG4_TX_BYTES)   # 508,052
 CFG4_STRIDE = (CFG4_BATCH_BYTES + 255) & ~255
 
 
-PROFILE_ROUND = "r04"   # profiles/<round>/summary.json: rocprofv3 PMC passes of this build
+PROFILE_ROUND = "r05"   # profiles/<round>/summary.json: rocprofv3 PMC passes of this build
 
 
 def profile_counters(*kernel_names: str):
@@ -1132,7 +1132,8 @@ def main():
         if digest is not None:
             digest["cpu_baseline"] = cpu_baseline_digest(args.cpu_budget / 2)
 
-    vpc = profile_counters("nwc::k_verify<true, false, false>", "nwc::k_verify<true, false>")
+    vpc = profile_counters("nwc::k_verify<true, false, false, false>", "nwc::k_verify<true, false, false>",
+                           "nwc::k_verify<true, false>")
     dpc = profile_counters("nwc::" + digest["kernel"]) if digest is not None else None
     if digest is not None and dpc:
         digest["traffic"] = dpc["traffic"]
