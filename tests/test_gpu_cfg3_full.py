@@ -5,7 +5,8 @@ them.  Certificate::verify's batch check (primary/src/messages.rs:189-215 -> cry
 206-219) runs through every entry that decides it:
 
 - the uncached per-vote leaves (launch keys off): nwc_dev_verify + nwc_dev_cert_reduce;
-- dalek's batch equation over sub-batches (nwc_dev_verify_batch_straus);
+- dalek's batch equation over sub-batches (nwc_dev_verify_batch_straus), and as Pippenger MSM
+  groups (nwc_dev_verify_batch_msm) through its skip policy's first calls;
 - the launch keys (no nwc_set_committee): the first call, where the keys join and their combs are
   built, and the steady state;
 - the crate's host entry nwc_verify_batch_many from pageable host buffers.
@@ -66,6 +67,14 @@ def test_cfg3_device_entries(cfg3):
         _check(*device.cert_reduce(leaf, w["offs"], M * Q), w)
         straus = device.verify_batch_straus(w["cdig"], w["offs"], w["msg_index"], w["pks"], w["sigs"])
         _check(*device.cert_reduce(straus, w["offs"], M * Q), w)
+        # the Pippenger groups: every group holds bad votes at 1 %, so the first call fails them all
+        # into the Straus sub-batches and the next ones skip the equation (the policy's cycle)
+        for call in range(3):
+            s0 = device.msm_stats()
+            msm = device.verify_batch_msm(w["cdig"], w["offs"], w["msg_index"], w["pks"], w["sigs"])
+            _check(*device.cert_reduce(msm, w["offs"], M * Q), w)
+            s1 = device.msm_stats()
+            assert s1[0] == s0[0], (call, s0, s1)   # no group passes with a bad vote in it
         _lib.diag_set("launch_keys", 1)
         for call in ("first", "steady"):
             lk = device.verify(w["cdig"], w["pks"], w["sigs"], strict=False, msg_index=w["msg_index"])
