@@ -2375,7 +2375,7 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
   std::vector<size_t> cuts{0};
   const uint64_t lo = std::min<uint64_t>((uint64_t)8 << 20, msg_chunk);
   if (staged && msg_chunk && total >= 4 * lo) {
-    uint64_t at = 0, next = 2 * lo;
+    uint64_t at = 0, next = std::min<uint64_t>(msg_chunk, 2 * lo);
     while (total - at > 2 * lo) {
       const uint64_t want = std::max(lo, std::min(next, (total - at) / 2));
       const size_t cm = (size_t)(std::lower_bound(hoff.begin(), hoff.end(), at + want) - hoff.begin());

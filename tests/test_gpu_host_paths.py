@@ -110,10 +110,13 @@ def test_sanitize_messages_host_staged():
     _sanitize_tiled_golden()
 
 
-def test_sanitize_messages_host_chunks():
+@pytest.mark.parametrize("mode", [{}, {"NWC_LEAF_ROUNDS": "1"}, {"NWC_LEAF_STREAM": "0"}],
+                         ids=["leaves-per-chunk", "leaves-in-rounds", "leaves-behind-parse"])
+def test_sanitize_messages_host_chunks(mode):
     """The same batch in 1-MB pipelined chunks (NWC_MSG_CHUNK, read once per process: a child
-    process): ~8 chunks cut on message boundaries, each parsed and verified while the next one
-    crosses PCIe, codes and digests unchanged."""
+    process): ~8 chunks cut on message boundaries sharing one 64-aligned vote counter, each parsed
+    while the previous one's leaves run (or behind them, or with the leaves in whole rounds of the
+    comb kernel's lanes), codes and digests unchanged."""
     import os
     import subprocess
     import sys
@@ -123,8 +126,10 @@ def test_sanitize_messages_host_chunks():
             "_sanitize_tiled_golden()\n"
             "print('done', flush=True)\n" % ROOT)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=ROOT,
-                       env=dict(os.environ, NWC_MSG_CHUNK=str(1 << 20)))
+                       env=dict(os.environ, NWC_MSG_CHUNK=str(1 << 20), NWC_HOST_TIMING="1", **mode))
     assert r.returncode == 0 and "done" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-3000:])
+    steps = [l for l in r.stderr.splitlines() if l.startswith("nwc sanitize steps:")]
+    assert steps and all(l.count("parse queued") >= 4 for l in steps), r.stderr[-2000:]   # several chunks
 
 
 def _sanitize_tiled_golden():
