@@ -291,12 +291,14 @@ __global__ __launch_bounds__(64, 2) void k_verify_msm(MsmArgs a) {
         c = tsum >> 32;
       }
       sum[8] = (u32)c;
+      // lo = sum mod 2^130, hi = sum >> 130 (< 2^135)
       u32 lo[5], hi[5];
-      _Pragma("unroll") for (int i = 0; i < 5; ++i) {
-        lo[i] = i < 4 ? sum[i] : (sum[4] & 3u);   // bits 0 .. 129
-        // bits 130 + 32 i .. : sum >> 130
-        hi[i] = (sum[4 + i] >> 2) | (i < 4 ? sum[5 + (i < 4 ? i : 0)] << 30 : 0u);
+      _Pragma("unroll") for (int i = 0; i < 4; ++i) {
+        lo[i] = sum[i];
+        hi[i] = (sum[4 + i] >> 2) | (sum[5 + i] << 30);
       }
+      lo[4] = sum[4] & 3u;
+      hi[4] = sum[8] >> 2;
       i32 dl[MSM_WIN], dh[MSM_WIN];
       msm_recode<MSM_WIN, 5>(lo, dl);
       msm_recode<MSM_WIN, 5>(hi, dh);
