@@ -15,28 +15,31 @@
 //     so every vote keeps exactly dalek's coefficient); then one lane per distinct key decompresses
 //     it and recodes its sum.
 //   phase 2, Pippenger over the group's points, 14 windows of 10 bits from the top (z_i < 2^128
-//     has digits in the low 13; a key's sum is split at 2^130 between A_j and 2^130 A_j): per window the points are counting-sorted by |digit| into
-//     512 buckets in LDS; lane l owns buckets 8l+1 .. 8l+8 and walks them from the top, adding
-//     each point into a running sum and, at each bucket boundary, the running sum into its local
-//     total (one addition per point and per bucket, as one merged event stream per lane so the
-//     SIMD stays busy).  The wavefront-level bucket reduction then needs, of all 64 lanes,
-//     sum_l local_l + 8 sum_l l S_l (S_l = lane l's running sum): an inclusive suffix scan of S
-//     over the lanes (6 DPP/shuffle steps) gives sum_l l S_l as the sum of the suffixes, so each
-//     lane adds local_l + 8 SS_l (SS_0 excluded) into its own Horner accumulator, and the 64
-//     accumulators are summed once, after the last window.
+//     has digits in the low 13; a key's sum is split at 2^130 between A_j and 2^130 A_j): per
+//     window the points are counting-sorted by |digit| into 512 buckets in LDS; lane l takes the
+//     contiguous buckets [c_l, c_(l+1)) that hold the l-th 64th of the window's events (a point
+//     each, a bucket end each), and walks them from the top as one merged event stream -- each
+//     point into a running sum, at each bucket's end the running sum into the lane's local total
+//     -- so every lane has about the same number of events whatever the digits' distribution.
+//     The wavefront-level bucket reduction: sum_b b B_b = sum_l local_l + sum_(l>=1) n_(l-1) SS_l,
+//     where SS is the inclusive suffix scan of the lanes' running sums (6 shuffle steps) and
+//     n_(l-1) the bucket count of the lane below (a short double-and-add); each lane adds its
+//     term into its own Horner accumulator, and the 64 accumulators are summed once, after the
+//     last window.
 //   phase 3: - (sum z_i s_i mod l) B from the radix-2^22 basepoint comb, the identity test.
 //
 // A group that passes sets its votes' leaf bits; one that fails -- a vote that does not parse or
-// decode, more than MSM_KMAX distinct keys, or the equation -- lists its votes for the exact
-// per-vote leaves (as k_verify_straus).  Semantics are the Straus entry's:
-// exact on the deterministic domain, dalek's ~1/ord acceptance on the randomized one.
+// decode, more than MSM_KMAX distinct keys, or the equation -- lists its votes for the Straus
+// sub-batches (list-mode k_verify_straus), whose failing sub-batches go to the exact per-vote
+// leaves.  Semantics are the Straus entry's: exact on the deterministic
+// domain, dalek's acceptance probabilities on the randomized one.
 #pragma once
 
 namespace nwc {
 
 constexpr int MSM_C = 10;                       // window bits
 constexpr int MSM_BUCKETS = 1 << (MSM_C - 1);   // |digit| in 1 .. 512
-constexpr int MSM_BW = MSM_BUCKETS / 64;        // buckets per lane
+constexpr int MSM_BW = MSM_BUCKETS / 64;        // buckets per lane in the counts' scan
 constexpr int MSM_RWIN = 13;                    // windows of z < 2^128 (130 bits)
 constexpr int MSM_WIN = 14;                     // windows of the group (a key's sum split at 2^130: < 2^135 each)
 constexpr int MSM_KSPLIT = 130;                 // key point j: sum mod 2^130 on A_j, sum >> 130 on 2^130 A_j
@@ -349,7 +352,8 @@ __global__ __launch_bounds__(64, 2) void k_verify_msm(MsmArgs a) {
           if (d) atomicAdd(&L.p2.cnt[(d < 0 ? -d : d) - 1], 1u);
         }
         __syncthreads();
-        // exclusive scan: lane l owns buckets [8l, 8l + 8)
+        // exclusive scan of the counts (lane l scans buckets 8l .. 8l + 7): cnt[b] and cur[b]
+        // become bucket b's start (the scatter below advances cur[b] to its end)
         u32 c8[MSM_BW], lsum = 0;
         _Pragma("unroll") for (int i = 0; i < MSM_BW; ++i) {
           c8[i] = L.p2.cnt[MSM_BW * lane + i];
@@ -360,10 +364,11 @@ __global__ __launch_bounds__(64, 2) void k_verify_msm(MsmArgs a) {
           const u32 y = (u32)__shfl_up((int)incl, o, 64);
           if ((int)lane >= o) incl += y;
         }
-        const u32 rstart = incl - lsum;
+        const u32 npts = (u32)__shfl((int)incl, 63, 64);   // the window's points
         {
-          u32 run = rstart;
+          u32 run = incl - lsum;
           _Pragma("unroll") for (int i = 0; i < MSM_BW; ++i) {
+            L.p2.cnt[MSM_BW * lane + i] = run;
             L.p2.cur[MSM_BW * lane + i] = run;
             run += c8[i];
           }
@@ -386,28 +391,62 @@ __global__ __launch_bounds__(64, 2) void k_verify_msm(MsmArgs a) {
           }
         }
         __syncthreads();
-        // cur[b] is now the end of bucket b.  The lane's events, from its top bucket down: each
-        // point of bucket b into `run`, then `loc` += `run` at the bucket's end
-        const u32 rend = L.p2.cur[MSM_BW * lane + MSM_BW - 1];
-        const u32 nev = (rend - rstart) + MSM_BW;
+        // Lane l takes the buckets [c_l, c_(l+1)) whose events (a point each, a bucket end each:
+        // bucket b's first event has index start(b) + b) fall in the l-th 64th of the window's
+        // npts + 512: every lane walks about the same number of events, whatever the digits'
+        // distribution (fixed 8-bucket ranges left 30 % of the event slots idle, and z's top
+        // window, whose digits all fall in the lower half, twice that)
+        const u32 nte = npts + (u32)MSM_BUCKETS;
+        auto start_of = [&](u32 b) -> u32 { return b < (u32)MSM_BUCKETS ? L.p2.cnt[b] : npts; };
+        auto first_bucket = [&](u32 l) -> u32 {   // min b in [0, 512] with start(b) + b >= l * nte / 64
+          const u32 target = (l * nte + 63) / 64;
+          u32 lo = 0, hi = MSM_BUCKETS;
+          _Pragma("unroll") for (int it = 0; it < 10; ++it) {
+            const u32 mid = (lo + hi) >> 1;
+            const bool up = lo < hi && start_of(mid) + mid < target;
+            lo = up ? mid + 1 : lo;
+            hi = (lo < hi && !up) ? mid : hi;
+          }
+          return lo;
+        };
+        const u32 c_lo = first_bucket(lane), c_hi = lane == 63 ? (u32)MSM_BUCKETS : first_bucket(lane + 1);
+        const u32 p_lo = start_of(c_lo), p_hi = start_of(c_hi);
+        const u32 nev = (p_hi - p_lo) + (c_hi - c_lo);
         u32 E = nev;
         _Pragma("unroll") for (int m = 32; m >= 1; m >>= 1) E = max(E, (u32)__shfl_xor((int)E, m, 64));
         E = __builtin_amdgcn_readfirstlane(E);
+        // the lane's events from its top bucket down: each point of bucket b into `run`, then
+        // `loc` += `run` at the bucket's end
         ge_p3 run = ge_p3_identity(), loc = ge_p3_identity();
-        int bi = MSM_BW - 1;
-        int pos = (int)rend - 1;
+        int bi = (int)c_hi - 1;
+        int pos = (int)p_hi - 1;
+        // an event's kind and point depend only on (bi, pos), not on the additions: the next
+        // event's 128-B point gather is issued before this event's arithmetic
+        auto next_event = [&](u32 ev, bool& act, bool& is_pt, u32& id, uint4 (&pv)[MSM_POINT_U4]) {
+          act = ev < nev;
+          is_pt = act && bi >= (int)c_lo && pos >= (int)start_of((u32)max(bi, 0));
+          id = is_pt ? (u32)L.p2.sorted[pos] : 0u;
+          const uint4* e = pts + (size_t)(id & 0x7FFFu) * MSM_POINT_U4;
+          _Pragma("unroll") for (int k = 0; k < (int)MSM_POINT_U4; ++k) pv[k] = e[k];
+        };
+        bool act_n, pt_n;
+        u32 id_n;
+        uint4 pn[MSM_POINT_U4];
+        next_event(0, act_n, pt_n, id_n, pn);
 #pragma unroll 1
         for (u32 ev = 0; ev < E; ++ev) {
-          const bool act = ev < nev;
-          const int bstart = bi > 0 ? (int)L.p2.cur[MSM_BW * lane + bi - 1] : (int)rstart;
-          const bool is_pt = act && bi >= 0 && pos >= bstart;
-          const u32 id = is_pt ? (u32)L.p2.sorted[pos] : 0u;
-          const uint4* e = pts + (size_t)(id & 0x7FFFu) * MSM_POINT_U4;
+          const bool act = act_n, is_pt = pt_n;
+          const u32 id = id_n;
+          uint4 pc[MSM_POINT_U4];
+          _Pragma("unroll") for (int k = 0; k < (int)MSM_POINT_U4; ++k) pc[k] = pn[k];
+          pos -= is_pt ? 1 : 0;
+          bi -= (act && !is_pt) ? 1 : 0;
+          if (ev + 1 < E) next_event(ev + 1, act_n, pt_n, id_n, pn);
           const bool neg = (id & 0x8000u) != 0;
           ge_cached q;
           {
-            const fe ypx = fe_unpack(e[0], e[1]), ymx = fe_unpack(e[2], e[3]), pz = fe_unpack(e[4], e[5]),
-                     t2d = fe_unpack(e[6], e[7]);
+            const fe ypx = fe_unpack(pc[0], pc[1]), ymx = fe_unpack(pc[2], pc[3]), pz = fe_unpack(pc[4], pc[5]),
+                     t2d = fe_unpack(pc[6], pc[7]);
             const ge_cached qr = ge_p3_to_cached(run);
             q.YpX = fe_select(qr.YpX, neg ? ymx : ypx, is_pt);
             q.YmX = fe_select(qr.YmX, neg ? ypx : ymx, is_pt);
@@ -418,19 +457,31 @@ __global__ __launch_bounds__(64, 2) void k_verify_msm(MsmArgs a) {
           const ge_p3 r = ge_p1p1_to_p3(ge_add_cached(tgt, q));
           run = p3_select(run, r, is_pt);
           loc = p3_select(loc, r, act && !is_pt);
-          pos -= is_pt ? 1 : 0;
-          bi -= (act && !is_pt) ? 1 : 0;
         }
-        // wavefront bucket reduction: sum_l loc_l + 8 sum_{l >= 1} SS_l, SS_l = sum_{k >= l} run_k
+        // Wavefront bucket reduction.  loc_l = sum over the lane's buckets of (b - c_l + 1) B_b,
+        // run_l = U_l = the sum of its points, so the window's sum_b (b + 1) B_b is
+        //   sum_l loc_l + sum_l c_l U_l = sum_l loc_l + sum_{l >= 1} (c_l - c_(l-1)) SS_l,
+        // SS_l = sum_{k >= l} U_k (Abel summation, c_0 = 0): an inclusive suffix scan of the
+        // running sums over the lanes (6 shuffle steps), then each lane's SS times the bucket count
+        // of the lane below it (a few doublings: the wave's largest count has ~4-7 bits)
         ge_p3 ss = run;
         _Pragma("unroll 1") for (int o = 1; o < 64; o <<= 1) {
           const ge_p3 other = shfl_down_p3(ss, o);
           const ge_p3 sum = p3_add(ss, other);
           ss = p3_select(ss, sum, (int)lane + o < 64);
         }
-        ss = p3_select(ss, ge_p3_identity(), lane == 0);
-        const ge_p3 y = p3_add(loc, p3_dbl_n(ss, MSM_C - 1 - 6));   // x 8 = MSM_BW
-        T = p3_add(T, y);
+        const u32 c_prev = (u32)__shfl_up((int)c_lo, 1, 64);
+        const u32 nb = lane == 0 ? 0u : c_lo - c_prev;
+        u32 nbmax = nb;
+        _Pragma("unroll") for (int m = 32; m >= 1; m >>= 1) nbmax = max(nbmax, (u32)__shfl_xor((int)nbmax, m, 64));
+        const int bits = 32 - __builtin_clz(__builtin_amdgcn_readfirstlane(nbmax) | 1u);
+        ge_p3 acc = ge_p3_identity();
+#pragma unroll 1
+        for (int k = bits - 1; k >= 0; --k) {
+          acc = p3_dbl_n(acc, 1);
+          acc = p3_select(acc, p3_add(acc, ss), ((nb >> k) & 1u) != 0);
+        }
+        T = p3_add(T, p3_add(loc, acc));
         __syncthreads();   // the window's LDS (counts, sorted) is rewritten by the next one
       }
       // the 64 lanes' accumulators
