@@ -30,6 +30,11 @@ bad2 = ctypes.create_string_buffer((int(offs[-1]) + 7) // 8)
 _lib.check(lib.nwc_verify_batch_straus_many(_lib.buf(dig), _lib.buf(offs), _lib.buf(p), _lib.buf(s), mc, cert2, bad2))
 out["cert_straus"] = np.frombuffer(cert2.raw, np.uint8).copy()
 out["bad_straus"] = np.frombuffer(bad2.raw, np.uint8).copy()
+cert3 = ctypes.create_string_buffer((mc + 7) // 8)
+bad3 = ctypes.create_string_buffer((int(offs[-1]) + 7) // 8)
+_lib.check(lib.nwc_verify_batch_msm_many(_lib.buf(dig), _lib.buf(offs), _lib.buf(p), _lib.buf(s), mc, cert3, bad3))
+out["cert_msm"] = np.frombuffer(cert3.raw, np.uint8).copy()
+out["bad_msm"] = np.frombuffer(bad3.raw, np.uint8).copy()
 blob, boffs = d["blob"], d["boffs"]
 nb = len(boffs) - 1
 o32 = np.zeros((nb, 32), np.uint8)

@@ -1,6 +1,7 @@
 """The library's multi-device host paths on a one-GPU box: NWC_VIRTUAL_DEVICES=k (3, and 8 = one
 node's width) makes nwc_init open k contexts on the GPU, so nwc_verify_strict_many's shard threads and bitmap merge,
-nwc_verify_batch_many's and nwc_verify_batch_straus_many's certificate cuts and nwc_sha512_trunc32_many's
+nwc_verify_batch_many's, nwc_verify_batch_straus_many's and nwc_verify_batch_msm_many's certificate cuts
+and nwc_sha512_trunc32_many's
 split all run as with three
 GPUs.  Outputs must equal the oracle's bit for bit, including verdicts that
 straddle the shard boundaries."""
@@ -62,6 +63,9 @@ def test_contexts_match_oracle(oracle, tmp_path, contexts):
     # the Straus host entry over the same certificate cuts (honest keys: the deterministic domain)
     assert (bits(got2["cert_straus"], len(sizes)) == ocert).all()
     assert (bits(got2["bad_straus"], n) == obad).all()
+    # and the Pippenger host entry (its groups fall back to the sub-batches, then the leaves)
+    assert (bits(got2["cert_msm"], len(sizes)) == ocert).all()
+    assert (bits(got2["bad_msm"], n) == obad).all()
     raw = blob.tobytes()
     for i in range(len(lens)):
         assert got["digests"][i].tobytes() == hashlib.sha512(raw[boffs[i]:boffs[i + 1]]).digest()[:32], i
@@ -101,6 +105,6 @@ def test_contexts_device_vote_index(tmp_path):
     assert int(got["devices"][0]) == 3
     bits = lambda raw, k: np.unpackbits(raw, bitorder="little")[:k].astype(bool)  # noqa: E731
     exp_cert = np.bincount(vote_cert[bad], minlength=m) == 0
-    for c, b in (("cert", "bad"), ("cert_straus", "bad_straus")):
+    for c, b in (("cert", "bad"), ("cert_straus", "bad_straus"), ("cert_msm", "bad_msm")):
         assert (bits(got[b], nv) == bad).all(), (b, np.nonzero(bits(got[b], nv) != bad)[0][:10])
         assert (bits(got[c], m) == exp_cert).all(), (c, np.nonzero(bits(got[c], m) != exp_cert)[0][:10])
