@@ -18,6 +18,7 @@
  *                                          percentiles over calls warm..calls-1
  *   T <m> <offsets m+1>, votes and digests as C -> "T <rc> <cert bitmap> <bad bitmap>"
  *                                          (nwc_verify_batch_straus_many)
+ *   P <m> ..., as T                          -> "P <rc> ..."  (nwc_verify_batch_msm_many)
  *   Q <n>, then n lines <pk32 stake nworkers wid...>  -> "Q <rc>"  (nwc_set_committee_config)
  *   M <m> <gc_round> <target72 | ->, then m lines <msg hex> -> "M <rc> <code,kind,digest32>..."
  *                                          (nwc_sanitize_messages)
@@ -228,7 +229,7 @@ int main(void) {
       g_vs = sigs;
       g_vbits = bits;
       g_vn = rc == 0 ? n : 0;
-    } else if (tok[0] == 'C' || tok[0] == 'T') {
+    } else if (tok[0] == 'C' || tok[0] == 'T' || tok[0] == 'P') {
       const char kind = tok[0];
       const char* cnt = strtok(NULL, " \n");
       if (!cnt) return 3;
@@ -256,8 +257,9 @@ int main(void) {
       }
       unsigned char* cert = calloc(mc / 8 + 1, 1);
       unsigned char* badv = calloc(nv / 8 + 1, 1);
-      rc = kind == 'C' ? nwc_verify_batch_many(dig, offs, pks, sigs, mc, cert, badv)
-                       : nwc_verify_batch_straus_many(dig, offs, pks, sigs, mc, cert, badv);
+      rc = kind == 'C'   ? nwc_verify_batch_many(dig, offs, pks, sigs, mc, cert, badv)
+           : kind == 'T' ? nwc_verify_batch_straus_many(dig, offs, pks, sigs, mc, cert, badv)
+                         : nwc_verify_batch_msm_many(dig, offs, pks, sigs, mc, cert, badv);
       printf("%c %d ", kind, rc);
       puthex(cert, (mc + 7) / 8);
       printf(" ");

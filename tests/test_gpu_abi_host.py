@@ -2,8 +2,8 @@
 process, as in the Rust `crypto` shim of INTEGRATION.md.  Golden strict verdicts, the reference
 batch cases with their bad-vote bitmaps, and SHA-512 digests, through nwc_verify_strict /
 nwc_verify_batch / nwc_sha512_trunc32_many; and, in the AddressSanitizer + UBSan build, every
-host entry with threads or queues behind it: sharded strict and certificate calls, the Straus
-batch entry, the message pipeline, the worker digester (stages, receive arena, a failing group)
+host entry with threads or queues behind it: sharded strict and certificate calls, the Straus and
+MSM batch entries, the message pipeline, the worker digester (stages, receive arena, a failing group)
 and a digester streaming while other threads verify on the same device."""
 import hashlib
 import os
@@ -168,6 +168,11 @@ def test_c_host_under_asan(oracle, golden_verify, golden_batch):
     lines += ["%s %s" % (p.tobytes().hex(), s.tobytes().hex()) for p, s in zip(vp, vs)]
     lines += [d.tobytes().hex() for d in dig]
     want.append("T" + want[-1][1:])
+    # and as Pippenger groups (their failing groups through the sub-batches, then the leaves)
+    lines.append("P %d %s" % (len(sizes), " ".join(str(int(o)) for o in offs)))
+    lines += ["%s %s" % (p.tobytes().hex(), s.tobytes().hex()) for p, s in zip(vp, vs)]
+    lines += [d.tobytes().hex() for d in dig]
+    want.append("P" + want[-1][1:])
     lines.append("X 4 3")
     want.append("X 0")
     # Core::sanitize_* from wire bytes on the reference's fixtures and the restated negatives
