@@ -16,16 +16,16 @@
 //     it and recodes its sum.
 //   phase 2, Pippenger over the group's points, 14 windows of 10 bits from the top (z_i < 2^128
 //     has digits in the low 13; a key's sum is split at 2^130 between A_j and 2^130 A_j): per
-//     window the points are counting-sorted by |digit| into 512 buckets in LDS; lane l takes the
-//     contiguous buckets [c_l, c_(l+1)) that hold the l-th 64th of the window's events (a point
-//     each, a bucket end each), and walks them from the top as one merged event stream -- each
-//     point into a running sum, at each bucket's end the running sum into the lane's local total
-//     -- so every lane has about the same number of events whatever the digits' distribution.
-//     The wavefront-level bucket reduction: sum_b b B_b = sum_l local_l + sum_(l>=1) n_(l-1) SS_l,
-//     where SS is the inclusive suffix scan of the lanes' running sums (6 shuffle steps) and
-//     n_(l-1) the bucket count of the lane below (a short double-and-add); each lane adds its
-//     term into its own Horner accumulator, and the 64 accumulators are summed once, after the
-//     last window.
+//     window the points are counting-sorted by |digit| into 512 buckets in LDS.  The window's
+//     events in walking order -- for each bucket from the top, its points, then its end -- are
+//     cut into 64 equal segments, lane l walking the l-th from the bottom: each point into a
+//     running sum, at each bucket end the running sum into the lane's local total, so every lane
+//     has the same number of events whatever the digits' distribution (a bucket may be shared by
+//     two lanes).  The wavefront-level bucket reduction: sum_b b B_b = sum_l local_l +
+//     sum_l beta_l SS_(l+1), where SS is the inclusive suffix scan of the lanes' running sums
+//     (6 shuffle steps) and beta_l the bucket ends in lane l's segment (a short double-and-add);
+//     each lane adds its term into its own Horner accumulator, and the 64 accumulators are summed
+//     once, after the last window.
 //   phase 3: - (sum z_i s_i mod l) B from the radix-2^22 basepoint comb, the identity test.
 //
 // A group that passes sets its votes' leaf bits; one that fails -- a vote that does not parse or
@@ -391,40 +391,40 @@ __global__ __launch_bounds__(64, 2) void k_verify_msm(MsmArgs a) {
           }
         }
         __syncthreads();
-        // Lane l takes the buckets [c_l, c_(l+1)) whose events (a point each, a bucket end each:
-        // bucket b's first event has index start(b) + b) fall in the l-th 64th of the window's
-        // npts + 512: every lane walks about the same number of events, whatever the digits'
-        // distribution (fixed 8-bucket ranges left 30 % of the event slots idle, and z's top
-        // window, whose digits all fall in the lower half, twice that)
+        // The window's events in walking order D: for b = 511 .. 0, bucket b's points (from its
+        // end down), then its end.  Lane l walks D[S_l, S_(l+1)) with S_l = (63 - l) * nte / 64:
+        // every lane the same number of events whatever the digits' distribution (a lane may start
+        // inside a bucket; a bucket may be shared by two lanes).  D index of bucket b's first event:
+        // Dpos(b) = (npts - end(b)) + (511 - b), decreasing in b.
         const u32 nte = npts + (u32)MSM_BUCKETS;
-        auto start_of = [&](u32 b) -> u32 { return b < (u32)MSM_BUCKETS ? L.p2.cnt[b] : npts; };
-        auto first_bucket = [&](u32 l) -> u32 {   // min b in [0, 512] with start(b) + b >= l * nte / 64
-          const u32 target = (l * nte + 63) / 64;
-          u32 lo = 0, hi = MSM_BUCKETS;
-          _Pragma("unroll") for (int it = 0; it < 10; ++it) {
+        const u32 s_lo = (u32)(((uint64_t)(63 - lane) * nte) / 64), s_hi = (u32)(((uint64_t)(64 - lane) * nte) / 64);
+        auto start_of = [&](int b) -> int { return (int)L.p2.cnt[b]; };   // bucket b's first sorted position
+        auto end_of = [&](int b) -> int { return (int)L.p2.cur[b]; };     // one past its last
+        auto dpos = [&](u32 b) -> u32 { return (npts - (u32)end_of((int)b)) + ((u32)MSM_BUCKETS - 1u - b); };
+        u32 bfirst = 0;   // min b in [0, 511] with Dpos(b) <= s_lo (b = 511 always qualifies)
+        {
+          u32 lo = 0, hi = MSM_BUCKETS - 1;
+          _Pragma("unroll") for (int it = 0; it < 9; ++it) {
             const u32 mid = (lo + hi) >> 1;
-            const bool up = lo < hi && start_of(mid) + mid < target;
-            lo = up ? mid + 1 : lo;
-            hi = (lo < hi && !up) ? mid : hi;
+            const bool le = dpos(mid) <= s_lo;
+            hi = (lo < hi && le) ? mid : hi;
+            lo = (lo < hi && !le) ? mid + 1 : lo;
           }
-          return lo;
-        };
-        const u32 c_lo = first_bucket(lane), c_hi = lane == 63 ? (u32)MSM_BUCKETS : first_bucket(lane + 1);
-        const u32 p_lo = start_of(c_lo), p_hi = start_of(c_hi);
-        const u32 nev = (p_hi - p_lo) + (c_hi - c_lo);
+          bfirst = lo;
+        }
+        const u32 nev = s_hi - s_lo;
         u32 E = nev;
         _Pragma("unroll") for (int m = 32; m >= 1; m >>= 1) E = max(E, (u32)__shfl_xor((int)E, m, 64));
         E = __builtin_amdgcn_readfirstlane(E);
-        // the lane's events from its top bucket down: each point of bucket b into `run`, then
-        // `loc` += `run` at the bucket's end
+        // the lane's events: each point into `run`, at a bucket's end `loc` += `run`
         ge_p3 run = ge_p3_identity(), loc = ge_p3_identity();
-        int bi = (int)c_hi - 1;
-        int pos = (int)p_hi - 1;
+        int bi = (int)bfirst;
+        int pos = end_of(bi) - 1 - (int)(s_lo - dpos(bfirst));   // below start(bi): the bucket's end
         // an event's kind and point depend only on (bi, pos), not on the additions: the next
         // event's 128-B point gather is issued before this event's arithmetic
         auto next_event = [&](u32 ev, bool& act, bool& is_pt, u32& id, uint4 (&pv)[MSM_POINT_U4]) {
           act = ev < nev;
-          is_pt = act && bi >= (int)c_lo && pos >= (int)start_of((u32)max(bi, 0));
+          is_pt = act && bi >= 0 && pos >= start_of(max(bi, 0));
           id = is_pt ? (u32)L.p2.sorted[pos] : 0u;
           const uint4* e = pts + (size_t)(id & 0x7FFFu) * MSM_POINT_U4;
           _Pragma("unroll") for (int k = 0; k < (int)MSM_POINT_U4; ++k) pv[k] = e[k];
@@ -458,20 +458,27 @@ __global__ __launch_bounds__(64, 2) void k_verify_msm(MsmArgs a) {
           run = p3_select(run, r, is_pt);
           loc = p3_select(loc, r, act && !is_pt);
         }
-        // Wavefront bucket reduction.  loc_l = sum over the lane's buckets of (b - c_l + 1) B_b,
-        // run_l = U_l = the sum of its points, so the window's sum_b (b + 1) B_b is
-        //   sum_l loc_l + sum_l c_l U_l = sum_l loc_l + sum_{l >= 1} (c_l - c_(l-1)) SS_l,
-        // SS_l = sum_{k >= l} U_k (Abel summation, c_0 = 0): an inclusive suffix scan of the
-        // running sums over the lanes (6 shuffle steps), then each lane's SS times the bucket count
-        // of the lane below it (a few doublings: the wave's largest count has ~4-7 bits)
+        // Wavefront bucket reduction.  Every bucket end after lane l's segment counts its running
+        // sum U_l once more: m_l = bi + 1 of them (the lane stopped before bucket bi's end), so the
+        // window's sum_b (b + 1) B_b = sum_l loc_l + sum_l m_l U_l
+        //                            = sum_l loc_l + sum_l beta_l SS_(l+1)   (Abel summation),
+        // beta_l = m_(l+1) - m_l = the bucket ends in lane l's own segment (m_64 = 512) and
+        // SS_(l+1) = sum_(k > l) U_k: an inclusive suffix scan of the running sums over the lanes
+        // (6 shuffle steps), shifted by one lane, times beta_l (a short double-and-add: ~8, at most
+        // 9 bits)
         ge_p3 ss = run;
         _Pragma("unroll 1") for (int o = 1; o < 64; o <<= 1) {
           const ge_p3 other = shfl_down_p3(ss, o);
           const ge_p3 sum = p3_add(ss, other);
           ss = p3_select(ss, sum, (int)lane + o < 64);
         }
-        const u32 c_prev = (u32)__shfl_up((int)c_lo, 1, 64);
-        const u32 nb = lane == 0 ? 0u : c_lo - c_prev;
+        ss = p3_select(shfl_down_p3(ss, 1), ge_p3_identity(), lane == 63);   // SS_(l+1)
+        const u32 m_l = (u32)(bi + 1);
+        // (the shuffle outside the select: a shuffle inside a divergent branch reads the lanes
+        // that skip it as 0)
+        const u32 m_next = (u32)__shfl_down((int)m_l, 1, 64);
+        const u32 m_up = lane == 63 ? (u32)MSM_BUCKETS : m_next;
+        const u32 nb = m_up - m_l;
         u32 nbmax = nb;
         _Pragma("unroll") for (int m = 32; m >= 1; m >>= 1) nbmax = max(nbmax, (u32)__shfl_xor((int)nbmax, m, 64));
         const int bits = 32 - __builtin_clz(__builtin_amdgcn_readfirstlane(nbmax) | 1u);
