@@ -79,7 +79,7 @@ pub fn verify_batch(digest: &[u8; 32], public_keys: &[[u8; 32]], signatures: &[[
 /// per-certificate verdicts and the bad-vote set.  `dalek_batch = false`: the exact per-vote leaves
 /// (deterministic; Err on dalek's randomized domain); `true`: dalek's own random-linear-combination
 /// equation as a Pippenger MSM per group of votes, groups that fail re-decided by sub-batches of
-/// ~12 votes and those by the leaves (2.8x the leaves on clean traffic without a key cache; dalek's
+/// ~12 votes and those by the leaves (3.5x the leaves on clean traffic without a key cache; dalek's
 /// probabilities on the randomized domain).  Returns (certificate ok, vote bad) as bitmaps.
 pub fn verify_batch_many(digests: &[[u8; 32]], offsets: &[u32], public_keys: &[[u8; 32]], signatures: &[[u8; 64]],
                          dalek_batch: bool) -> (Vec<u8>, Vec<u8>) {
