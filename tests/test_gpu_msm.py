@@ -220,3 +220,40 @@ def test_skip_policy_on_a_high_bad_rate(oracle):
         assert per_call == [(0, groups)] * 7 + [(groups, 0)] * 2, per_call
     finally:
         _lib.diag_set("msm_group", 0)
+
+
+def test_launches_above_the_cap_run_in_pieces():
+    """NWC_VERIFY_MAX_LAUNCH (read once per process: a child) set to 65,536 votes: a 201k-vote call
+    of the MSM and Straus entries runs as four consecutive launches, each with its own groups or
+    sub-batches, fallback lists and leaf words; verdicts equal the construction (1 % of the votes
+    signed over another digest)."""
+    import os
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    code = r'''
+import sys; sys.path.insert(0, %r)
+import numpy as np, torch
+from narwhal_amd import device
+M, Q = 3000, 67
+nv = M * Q
+cdig = device.derive32(b"cap-cert", 0, M)
+seeds = device.derive32(b"cap-seed", 0, 100)
+g = torch.Generator(device="cuda"); g.manual_seed(7)
+who = torch.randint(0, 100, (nv,), device="cuda", generator=g)
+bad = torch.rand(nv, device="cuda", generator=g) < 0.01
+mi = torch.arange(M, device="cuda", dtype=torch.int32).repeat_interleave(Q)
+signed = cdig[mi.long()].clone(); signed[bad, 3] ^= 1
+pks, sigs = device.keygen_sign(seeds[who], signed)
+offs = torch.arange(M + 1, device="cuda", dtype=torch.int32) * Q
+want_bad = bad.cpu().numpy(); want_cert = ~want_bad.reshape(M, Q).any(axis=1)
+for f in (device.verify_batch_msm, device.verify_batch_straus):
+    cw, bw = device.cert_reduce(f(cdig, offs, mi, pks, sigs), offs, nv)
+    torch.cuda.synchronize()
+    assert (device.unpack_bits(bw, nv) == want_bad).all(), f.__name__
+    assert (device.unpack_bits(cw, M) == want_cert).all(), f.__name__
+print("done", flush=True)
+''' % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=ROOT,
+                       env=dict(os.environ, NWC_VERIFY_MAX_LAUNCH="65536"))
+    assert r.returncode == 0 and "done" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-3000:])
