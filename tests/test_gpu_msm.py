@@ -257,3 +257,31 @@ print("done", flush=True)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=ROOT,
                        env=dict(os.environ, NWC_VERIFY_MAX_LAUNCH="65536"))
     assert r.returncode == 0 and "done" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-3000:])
+
+
+@pytest.mark.parametrize("nkeys", [126, 127])
+def test_key_table_capacity_boundary(oracle, nkeys):
+    """One group of 2,048 clean votes over exactly nkeys distinct keys: 126 (MSM_KMAX) fit the LDS
+    key table and the group passes by the equation; 127 overflow it, and the group is decided by
+    the fallback -- verdicts exact either way (nwc_msm_stats tells which)."""
+    from narwhal_amd import _lib
+    rng = np.random.default_rng(61 + nkeys)
+    n = 2048
+    kseeds = rng.integers(0, 256, (nkeys, 32), dtype=np.uint8)
+    who = np.concatenate([np.arange(nkeys), rng.integers(0, nkeys, n - nkeys)])
+    m = 64
+    dig = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    offs = (np.arange(m + 1) * (n // m)).astype(np.int64)
+    pks, sigs = oracle.keygen_sign_many(kseeds[who], np.repeat(dig, n // m, axis=0))
+    _lib.diag_set("msm_group", 2048)
+    try:
+        s0 = _stats()
+        cert, bad = _run(dig, offs, pks, sigs)
+        s1 = _stats()
+    finally:
+        _lib.diag_set("msm_group", 0)
+    assert cert.all() and not bad.any()
+    if nkeys <= 126:
+        assert (s1[0] - s0[0], s1[1] - s0[1], s1[2] - s0[2]) == (1, 0, 0), (s0, s1)
+    else:
+        assert (s1[0] - s0[0], s1[1] - s0[1], s1[2] - s0[2]) == (0, 1, 1), (s0, s1)
