@@ -1127,6 +1127,8 @@ struct CombArgs {
   const ge_niels_pad* comb16;      // radix-2^16 basepoint comb (COMB16_TOTAL entries; k_verify_comb)
   uint8_t* vbytes;                 // latency kernel, host-mapped: per equation bit0 = valid, bit1 = key
                                    // missing (plain byte stores; nullptr = verdict words + count)
+  uint32_t list_base;              // added to the equation index a comb kernel lists (a call-wide list
+                                   // over consecutive launches, nwc_api.hip LV_DEFER_LIST)
 };
 
 __device__ __forceinline__ void load_inputs(const VerifyArgs& a, uint64_t i, u32 mw[8], u32 aw[8], u32 sgw[16]) {
@@ -1476,7 +1478,7 @@ __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs c
       u32 mw[8], aw[8], sgw[16];
       load_inputs(a, active ? i : 0, mw, aw, sgw);
       const int key = committee_lookup(cm, aw);
-      if (active && key < 0) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;
+      if (active && key < 0) ca.list[atomicAdd(ca.count, 1u)] = ca.list_base + (uint32_t)i;
       const int kk = key < 0 ? 0 : key;
       u32 rw[8], sw[8];
       _Pragma("unroll") for (int q = 0; q < 8; ++q) { rw[q] = sgw[q]; sw[q] = sgw[8 + q]; }
@@ -1937,7 +1939,7 @@ __global__ __launch_bounds__(128) void k_verify_comb_wide(VerifyArgs a, CombArgs
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     } else {
       if (key < 0) {
-        if (ca.list) ca.list[atomicAdd(ca.count, 1u)] = (uint32_t)i;
+        if (ca.list) ca.list[atomicAdd(ca.count, 1u)] = ca.list_base + (uint32_t)i;
         else atomicOr(ca.count, 1u);   // latency launch: flag it, the host re-runs the general path
       }
       if (flags_ok && eq) atomicOr(reinterpret_cast<unsigned long long*>(a.out_bits) + (i >> 6), 1ull << (i & 63));

@@ -695,12 +695,34 @@ __global__ __launch_bounds__(256) void k_header_digests(MsgArgs a) {
 //                UnknownAuthority (first vote) -> CertificateRequiresQuorum -> InvalidSignature
 //                                                            (core.rs:338-346, messages.rs:189-215)
 //   vote:        Serialization -> TooOld -> UnexpectedVote -> UnknownAuthority -> InvalidSignature
-// The shared vote-slot counter of a chunked call rounded up to a multiple of 64 (<= cap).
-__global__ void k_align_slots(uint32_t* v_total, uint32_t cap) {
-  if (threadIdx.x == 0) {
-    const uint32_t v = (*v_total + 63u) & ~63u;
-    *v_total = v < cap ? v : cap;
+// The shared vote-slot counter of a chunked call rounded up to a multiple of 64 (<= cap).  The
+// skipped slots repeat the last vote parsed so far: a leaf launch over them then takes that
+// vote's path (its key is cached), where stale slot bytes sent their uncached keys to the
+// latency-bound list kernel, ~0.7 ms at the end of every chunked call (profiles/r05/wire_host.md).
+// Their verdicts are never read.  One block of 64 threads.
+__global__ void k_align_slots(uint32_t* v_total, uint32_t cap, uint8_t* __restrict__ v_pk, uint8_t* __restrict__ v_sig,
+                              uint32_t* __restrict__ v_msg) {
+  const uint32_t v0 = *v_total;
+  const uint32_t a = (v0 + 63u) & ~63u, v = a < cap ? a : cap;
+  if (v0 > 0) {
+    const uint4* pk = reinterpret_cast<const uint4*>(v_pk + 32 * (size_t)(v0 - 1));
+    const uint4* sg = reinterpret_cast<const uint4*>(v_sig + 64 * (size_t)(v0 - 1));
+    const uint4 p0 = pk[0], p1 = pk[1], s0 = sg[0], s1 = sg[1], s2 = sg[2], s3 = sg[3];
+    const uint32_t mi = v_msg[v0 - 1];
+    for (uint32_t j = v0 + threadIdx.x; j < v; j += blockDim.x) {
+      uint4* dp = reinterpret_cast<uint4*>(v_pk + 32 * (size_t)j);
+      uint4* ds = reinterpret_cast<uint4*>(v_sig + 64 * (size_t)j);
+      dp[0] = p0;
+      dp[1] = p1;
+      ds[0] = s0;
+      ds[1] = s1;
+      ds[2] = s2;
+      ds[3] = s3;
+      v_msg[j] = mi;
+    }
   }
+  __syncthreads();   // every thread has read the count
+  if (threadIdx.x == 0) *v_total = v;
 }
 
 __global__ void k_finalize_messages(const uint32_t* __restrict__ rec, const uint32_t* __restrict__ rec_n,

@@ -134,6 +134,7 @@ struct DevCtx {
   uint32_t* msm_stats = nullptr;       // groups passed / failed / key overflow (nwc_msm_stats)
   uint32_t* uc_list = nullptr;     // k_verify_comb: equations whose key is not cached
   uint32_t* uc_count = nullptr;
+  bool hold_lists = false;         // a call with a deferred list pending: ensure_scratch does not shrink the lists
   // k_verify per-lane table slots; reused by every launch, so launches that use it are
   // serialised across streams with `scratch_free` (recorded after each such launch).
   uint8_t* scratch = nullptr;
@@ -600,7 +601,7 @@ void free_lists(DevCtx& d) {
 
 int ensure_scratch(DevCtx& d, size_t bytes, uint64_t n) {
   const uint64_t want = n + n / 2 + 4096;
-  const bool shrink = d.fb_cap > 4 * want && list_bytes(d.fb_cap, d.ts_slot_count) > verify_keep_bytes();
+  const bool shrink = !d.hold_lists && d.fb_cap > 4 * want && list_bytes(d.fb_cap, d.ts_slot_count) > verify_keep_bytes();
   if (bytes <= d.scratch_cap && n <= d.fb_cap && !shrink) return 0;
   HIP_TRY(hipEventSynchronize(d.scratch_free));
   if (bytes > d.scratch_cap) {
@@ -744,11 +745,30 @@ int ensure_stager(DevCtx& d) {
 // and/or out_words is already zero (both let the latency path run as a single kernel)
 // LV_AUTO: the keys are in the auto cache; LV_STAMP: the headline kernel's clock-stamp build
 // (k_verify<.., STAMP>, nwc_diag_verify_clock)
-constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4, LV_STAMP = 8;
+// LV_DEFER_LIST: a launch on the committee-cache comb path (deferrable_list()) that only appends
+// its uncached equations, as list_base + i, to the call-wide list; the caller zeroed the list's
+// count and sized the lists (ensure_scratch) for the whole call before the first such launch, and
+// runs the list, fallback and torsion passes once over all of them (finish_deferred_list).  The
+// chunked sanitize pipeline: one set of those small launches per call instead of per chunk.
+constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4, LV_STAMP = 8, LV_DEFER_LIST = 16;
+
+// launch_verify's comb path over the committee cache for any n (what LV_DEFER_LIST needs)
+bool deferrable_list(const DevCtx& d) {
+  return verify_path() == VPath::Default && d.cm_n && d.cm_comb && d.comb16;
+}
+
+// NWC_FORCE_FALLBACK_EVERY: test hook, every k-th equation of the half-size kernels takes the fallback
+uint32_t force_fallback_every() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("NWC_FORCE_FALLBACK_EVERY");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+  }();
+  return v;
+}
 
 int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
-                  hipStream_t s, int flags = 0, uint8_t* vbytes = nullptr) {
+                  hipStream_t s, int flags = 0, uint8_t* vbytes = nullptr, uint64_t list_base = 0) {
   if (n == 0) return 0;
   if (n > verify_max_launch() && !vbytes) {
     // consecutive launches of at most NWC_VERIFY_MAX_LAUNCH equations (a multiple of 64: whole
@@ -758,7 +778,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     for (uint64_t lo = 0; lo < n; lo += step) {
       const uint64_t len = std::min(step, n - lo);
       if (int rc = launch_verify(d, msg_index ? msgs : msgs + 32 * lo * msg_stride, msg_index ? msg_index + lo : nullptr,
-                                 msg_stride, pks + 32 * lo, sigs + 64 * lo, len, strict, out_words + lo / 64, s, flags))
+                                 msg_stride, pks + 32 * lo, sigs + 64 * lo, len, strict, out_words + lo / 64, s, flags,
+                                 nullptr, list_base + lo))
         return rc;
     }
     return 0;
@@ -779,10 +800,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     HIP_TRY(hipGetLastError());
     return 0;
   }
-  static const uint32_t force_every = [] {
-    const char* e = std::getenv("NWC_FORCE_FALLBACK_EVERY");
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
-  }();
+  const uint32_t force_every = force_fallback_every();
   if (vbytes && !(flags & LV_ALL_CACHED)) {
     // zero-copy cold launch (the caller checked: no committee cache, n <= NWC_WIDE_MAX, default
     // path, cold kernel on): no scratch, no fallback launch, verdict bytes straight to the host
@@ -798,6 +816,9 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const bool lk = path == VPath::Default && !strict && !d.cm_n && d.comb16 && n >= nwc::LK_MIN_EQUATIONS &&
                   knobs().launch_keys.load() && !(flags & LV_AUTO);
   const bool comb = lk || (path == VPath::Default && d.cm_n && d.cm_comb && (n <= NWC_WIDE_MAX || d.comb16));
+  const bool defer = (flags & LV_DEFER_LIST) != 0;
+  if (defer && (lk || !comb || list_base + n > d.fb_cap || !deferrable_list(d)))
+    return set_err(NWC_ERR_ARG, "deferred list launch off the committee-cache comb path");
   if (comb && n <= NWC_WIDE_MAX && (flags & LV_ALL_CACHED)) {
     // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none).
     // The host checked every key against its view of the cache (set under g_cm_mu, like the
@@ -827,7 +848,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     gridc = (unsigned)std::min<uint64_t>(tiles, resident);
     need = std::max(need, (size_t)resident * 256 * nwc::COMB_BYTES_PER_LANE);
   }
-  if (int rc = ensure_scratch(d, need, n)) return rc;
+  // (deferred: n = the lists' capacity, so they are neither grown nor shrunk under the pending list)
+  if (int rc = ensure_scratch(d, need, defer ? d.fb_cap : n)) return rc;
   if (lk)
     if (int rc = lk_ensure(d, s)) return rc;
   HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
@@ -847,7 +869,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
                     d.fb_list, d.fb_count, force_every, cm};
   a.force_windows = knobs().force_windows.load();
   a.stamps = d.stamps;
-  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
+  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16, nullptr, (uint32_t)(defer ? list_base : 0)};
   const bool half = path != VPath::Full;
   // small batch-leaf launches outside the comb path: the keys' torsion test (one long serial
   // lane per new key) runs on the side stream beside the verification instead of after it
@@ -860,6 +882,17 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     HIP_TRY(hipStreamWaitEvent(d.side, d.ev_fork, 0));
     if (int rc = launch_torsion(d, pks, out_words, n, nullptr, nullptr, cm, d.side, 1, 1)) return rc;
     HIP_TRY(hipEventRecord(d.ev_join, d.side));
+  }
+  if (defer) {
+    if (n <= NWC_WIDE_MAX) {
+      HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
+      hipLaunchKernelGGL(nwc::k_verify_comb_wide, dim3((unsigned)n), dim3(128), 0, s, a, ca);
+    } else {
+      hipLaunchKernelGGL(nwc::k_verify_comb, dim3(gridc), dim3(256), 0, s, a, ca);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(d.scratch_free, s));
+    return 0;
   }
   if (half) HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
   if (comb) {
@@ -906,6 +939,38 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     if (int rc = launch_torsion(d, pks, out_words, n, comb ? d.uc_list : nullptr, comb ? d.uc_count : nullptr, cm, s))
       return rc;
   }
+  HIP_TRY(hipEventRecord(d.scratch_free, s));
+  return 0;
+}
+
+// The passes LV_DEFER_LIST launches left out, once over equations [0, n) of the arrays they were
+// launched on (their list holds indices into these): the uncached equations' half-size list
+// launch, its fallback and (batch leaves) the torsion pass over the same list.
+int finish_deferred_list(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
+                         const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
+                         hipStream_t s) {
+  if (n == 0) return 0;
+  if (!deferrable_list(d) || n > d.fb_cap) return set_err(NWC_ERR_ARG, "deferred list finish off the comb path");
+  const uint64_t tiles = (n + 255) / 256;
+  const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * NWC_VERIFY_GRID_MULT;
+  const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
+  if (int rc = ensure_scratch(d, (size_t)cap * 256 * 2 * nwc::TAB_BYTES_PER_LANE, d.fb_cap)) return rc;
+  HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
+  const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
+  nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24, d.scratch,
+                    d.fb_list, d.fb_count, force_fallback_every(), cm};
+  a.force_windows = knobs().force_windows.load();
+  a.stamps = d.stamps;
+  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
+  HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
+  nwc::VerifyArgs l = a;
+  l.committee.n = 0;
+  hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3(grid), dim3(256), 0, s, l, ca);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(grid < 16u ? grid : 16u), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  if (!strict)
+    if (int rc = launch_torsion(d, pks, out_words, n, d.uc_list, d.uc_count, cm, s)) return rc;
   HIP_TRY(hipEventRecord(d.scratch_free, s));
   return 0;
 }
@@ -2132,17 +2197,19 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
 // Device part of nwc_sanitize_messages: messages in HBM (ddata 4-byte aligned with >= 16 bytes
 // of readable padding, doff device u64[m+1] relative to ddata, `total` bytes), parsed as the
 // chunks cuts[k] .. cuts[k+1] (whole messages).  `chunk_ready(k)`, when given, returns once chunk
-// k's bytes are on their way and stream s waits for them (the host path's copies).  The chunks
-// share one vote-slot counter, so the votes of the chunks parsed so far are contiguous; after each
-// parse the host reads the count and launches the leaves of whole rounds of the leaf kernel's
-// resident lanes (a partial round costs a full one's time), on the side stream beside the next
-// chunk's parse, and the rest after the last chunk.  The strict equations (headers' and votes'
+// k's bytes are on their way and stream s waits for them (the host path's copies);
+// `chunk_queued(k)` tells without waiting whether they are, and chunk k's parse is then queued
+// before the host waits for chunk k - 1's count.  The chunks share one vote-slot counter, so the
+// votes of the chunks parsed so far are contiguous; after each parse the host reads the count and
+// launches those votes' leaves (NWC_LEAF_ROUNDS: in whole rounds of the leaf kernel's resident
+// lanes) on the side stream beside the next chunk's parse, and the rest after the last chunk.  The strict equations (headers' and votes'
 // own signatures) of all chunks but the last run while the last one crosses PCIe; the header
 // digests and the final codes run once over all m messages.
 static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total,
                         const std::vector<size_t>& cuts, uint64_t gc_round, const uint8_t* vote_target, int32_t* dcodes,
                         uint8_t* ddigests, uint32_t* drec, hipStream_t s,
-                        const std::function<int(size_t)>& chunk_ready = nullptr) {
+                        const std::function<int(size_t)>& chunk_ready = nullptr,
+                        const std::function<bool(size_t)>& chunk_queued = nullptr) {
   const size_t nch = cuts.size() - 1;
   // a vote list is allocated only when wholly inside its message (>= 72 B per vote)
   const uint64_t vt = total / 72 + 1 + (nch > 1 ? 64 * nch : 0);   // + the 64-slot alignment of each chunk
@@ -2206,6 +2273,26 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   }();
   const bool chunked = nch > 1;
   const hipStream_t ls = chunked && leaf_side ? d.side : s;
+  // the leaf launches of a chunked call on the committee-cache comb path only list their uncached
+  // equations (LV_DEFER_LIST); the list's half-size, fallback and torsion passes run once, after
+  // the leaves queued before the first strict launch (which reuses the list), instead of ~8 small
+  // launches per chunk on the leaf stream (NWC_DEFER_LISTS=0: per launch, A/B)
+  static const bool defer_env = [] {
+    const char* e = std::getenv("NWC_DEFER_LISTS");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  const bool defer = chunked && defer_env && deferrable_list(d);
+  struct HoldLists {
+    DevCtx& d;
+    ~HoldLists() { d.hold_lists = false; }
+  } hold{d};
+  if (defer) {
+    if (int rc = ensure_scratch(d, 0, vt)) return rc;
+    d.hold_lists = true;
+    HIP_TRY(hipStreamWaitEvent(ls, d.scratch_free, 0));
+    HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), ls));
+  }
+  bool pending = false;   // deferred leaf launches whose list passes have not been queued
   HIP_TRY(hipMemsetAsync(a.v_total, 0, 4, s));
   HIP_TRY(hipMemsetAsync(a.v_msg, 0, 4 * vt, s));
   const nwc::Committee cm{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
@@ -2226,16 +2313,25 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   }();
   const uint64_t round = leaf_rounds ? std::max<uint64_t>(64, leaf_rounds * d.cus * d.comb_blocks_per_cu * 256) : 64;
   uint64_t launched = 0;   // votes [0, launched) have their leaf launch queued
-  auto leaves = [&](uint64_t upto) -> int {
+  auto leaves = [&](uint64_t upto, bool deferred) -> int {
     if (upto <= launched) return 0;
     const int rc = launch_verify(d, a.cdig, a.v_msg + launched, 0, a.v_pk + 32 * launched, a.v_sig + 64 * launched,
-                                 upto - launched, 0, lbits + launched / 64, ls);
+                                 upto - launched, 0, lbits + launched / 64, ls, deferred ? LV_DEFER_LIST : 0, nullptr,
+                                 launched);
+    pending = pending || deferred;
     launched = upto;
     mark("leaves queued");
     return rc;
   };
+  auto finish = [&]() -> int {
+    if (!pending) return 0;
+    pending = false;
+    return finish_deferred_list(d, a.cdig, a.v_msg, 0, a.v_pk, a.v_sig, launched, 0, lbits, ls);
+  };
   uint64_t nv = 0;
-  for (size_t k = 0; k < nch; ++k) {
+  size_t queued = 0;   // chunks whose parse is queued
+  auto queue_parse = [&]() -> int {
+    const size_t k = queued++;
     if (chunk_ready)
       if (int rc = chunk_ready(k)) return rc;
     mark("chunk ready");
@@ -2257,13 +2353,23 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     HIP_TRY(hipGetLastError());
     if (nch > 1) {
       // the next chunk's votes from a 64-slot boundary: every leaf launch starts on its own
-      // verdict word (the skipped slots belong to no message; their leaves are never read)
-      hipLaunchKernelGGL(nwc::k_align_slots, dim3(1), dim3(64), 0, s, a.v_total, (uint32_t)vt);
+      // verdict word (the skipped slots repeat the last vote; their leaves are never read)
+      hipLaunchKernelGGL(nwc::k_align_slots, dim3(1), dim3(64), 0, s, a.v_total, (uint32_t)vt, a.v_pk, a.v_sig,
+                         a.v_msg);
       HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipMemcpyAsync(nv_host + k, a.v_total, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(d.ev_cnt[k], s));
     mark("parse queued");
+    return 0;
+  };
+  if (int rc = queue_parse()) return rc;
+  for (size_t k = 0; k < nch; ++k) {
+    // the next chunk's parse goes in before this chunk's count is awaited when its copy is already
+    // queued (no wait on the copier): it then follows this parse on the GPU without a host round
+    // trip in between
+    if (queued < nch && (!chunk_queued || chunk_queued(queued)))
+      if (int rc = queue_parse()) return rc;
     if (!chunked) continue;
     // the votes parsed so far, in whole rounds, on the leaf stream; the next chunk's copy goes
     // on in the copier thread meanwhile, and its parse runs beside these leaves
@@ -2274,13 +2380,17 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     // (before the last chunk every vote so far: the last leaf launch then holds only the last
     // chunk's votes)
     if (k + 2 == nch || (k + 1 < nch && !leaf_rounds))
-      if (int rc = leaves(nv)) return rc;
+      if (int rc = leaves(nv, defer)) return rc;
     if (k + 2 < nch && leaf_rounds)
-      if (int rc = leaves(launched + (nv - launched) / round * round)) return rc;
+      if (int rc = leaves(launched + (nv - launched) / round * round, defer)) return rc;
     // the strict equations of every chunk but the last while the last one crosses PCIe
     // (cuts[nch - 1] is a multiple of 64 messages: the two strict launches own their words)
-    if (k + 2 == nch)
+    if (k + 2 == nch) {
+      if (int rc = finish()) return rc;
       if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, cuts[k + 1], 1, sbits, ls)) return rc;
+    }
+    if (queued == k + 1 && queued < nch)
+      if (int rc = queue_parse()) return rc;
   }
   if (chunked) {
     // the Header::digest checks once, beside the last leaves (latency-bound: ~0.2 ms for any
@@ -2291,7 +2401,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     if (int rc = launch_verify(d, a.eq_msg + 32 * c0, nullptr, 1, a.eq_pk + 32 * c0, a.eq_sig + 64 * c0, m - c0, 1,
                                sbits + c0 / 64, ls))
       return rc;
-    if (int rc = leaves(nv)) return rc;
+    if (int rc = leaves(nv, false)) return rc;
     if (ls != s) {
       HIP_TRY(hipEventRecord(d.ev_msg, ls));
       HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
@@ -2306,7 +2416,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(d.ev_msg, d.side));
     HIP_TRY(hipEventSynchronize(d.ev_cnt[0]));
-    if (int rc = leaves(std::min<uint64_t>(nv_host[0], vt))) return rc;
+    if (int rc = leaves(std::min<uint64_t>(nv_host[0], vt), false)) return rc;
     HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
   }
   hipLaunchKernelGGL(nwc::k_finalize_messages, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a.rec,
@@ -2452,8 +2562,18 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
       if (e != hipSuccess) return set_err(NWC_ERR_DEVICE, "hipStreamWaitEvent: %s", hipGetErrorString(e));
       return 0;
     };
+    // NWC_PARSE_AHEAD=0: each chunk's parse queued only after the previous chunk's count (A/B)
+    static const bool parse_ahead = [] {
+      const char* e = std::getenv("NWC_PARSE_AHEAD");
+      return !(e && std::strcmp(e, "0") == 0);
+    }();
+    auto chunk_queued = [&](size_t k) -> bool {
+      if (!parse_ahead) return false;
+      std::lock_guard<std::mutex> g(cmu);
+      return recorded > k;
+    };
     int rc = sanitize_dev(d, ddata, doff, m, total, cuts, gc_round, vote_target, dcodes, ddig, drec, d.stream,
-                          chunk_ready);
+                          chunk_ready, chunk_queued);
     copier.join();   // the copier never waits on this thread: it runs through every chunk
     if (rc) {
       (void)hipStreamSynchronize(d.xfer);   // no copy still writes the arena when the call returns
