@@ -704,7 +704,7 @@ __global__ void k_align_slots(uint32_t* v_total, uint32_t cap, uint8_t* __restri
                               uint32_t* __restrict__ v_msg) {
   const uint32_t v0 = *v_total;
   const uint32_t a = (v0 + 63u) & ~63u, v = a < cap ? a : cap;
-  if (v0 > 0) {
+  if (v0 > 0 && v0 <= cap) {   // (a parse that overflowed the slots left the count above the cap)
     const uint4* pk = reinterpret_cast<const uint4*>(v_pk + 32 * (size_t)(v0 - 1));
     const uint4* sg = reinterpret_cast<const uint4*>(v_sig + 64 * (size_t)(v0 - 1));
     const uint4 p0 = pk[0], p1 = pk[1], s0 = sg[0], s1 = sg[1], s2 = sg[2], s3 = sg[3];

@@ -2202,9 +2202,9 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
 // before the host waits for chunk k - 1's count.  The chunks share one vote-slot counter, so the
 // votes of the chunks parsed so far are contiguous; after each parse the host reads the count and
 // launches those votes' leaves (NWC_LEAF_ROUNDS: in whole rounds of the leaf kernel's resident
-// lanes) on the side stream beside the next chunk's parse, and the rest after the last chunk.  The strict equations (headers' and votes'
-// own signatures) of all chunks but the last run while the last one crosses PCIe; the header
-// digests and the final codes run once over all m messages.
+// lanes) on the side stream beside the next chunk's parse, and the rest after the last chunk.
+// The strict equations (headers' and votes' own signatures) of all chunks but the last run while
+// the last one crosses PCIe; the header digests and the final codes run once over all m messages.
 static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total,
                         const std::vector<size_t>& cuts, uint64_t gc_round, const uint8_t* vote_target, int32_t* dcodes,
                         uint8_t* ddigests, uint32_t* drec, hipStream_t s,
