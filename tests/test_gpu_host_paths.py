@@ -110,13 +110,16 @@ def test_sanitize_messages_host_staged():
     _sanitize_tiled_golden()
 
 
-@pytest.mark.parametrize("mode", [{}, {"NWC_LEAF_ROUNDS": "1"}, {"NWC_LEAF_STREAM": "0"}],
-                         ids=["leaves-per-chunk", "leaves-in-rounds", "leaves-behind-parse"])
+@pytest.mark.parametrize("mode", [{}, {"NWC_LEAF_ROUNDS": "1"}, {"NWC_LEAF_STREAM": "0"}, {"NWC_DEFER_LISTS": "0"},
+                                  {"NWC_PARSE_AHEAD": "0"}],
+                         ids=["leaves-per-chunk", "leaves-in-rounds", "leaves-behind-parse", "lists-per-launch",
+                              "parse-after-count"])
 def test_sanitize_messages_host_chunks(mode):
     """The same batch in 1-MB pipelined chunks (NWC_MSG_CHUNK, read once per process: a child
     process): ~8 chunks cut on message boundaries sharing one 64-aligned vote counter, each parsed
     while the previous one's leaves run (or behind them, or with the leaves in whole rounds of the
-    comb kernel's lanes), codes and digests unchanged."""
+    comb kernel's lanes, or with each leaf launch's own uncached-list passes, or each parse queued
+    only after the previous chunk's count), codes and digests unchanged."""
     import os
     import subprocess
     import sys
