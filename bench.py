@@ -199,6 +199,49 @@ def cfg4_host_batch(b: int) -> bytes:
     return bytes(out)
 
 
+def cfg4_pool_host(b0: int, b1: int) -> np.ndarray:
+    """Pool batches b0 .. b1-1 built on the host with numpy, independently of the GPU construction
+    (make_cfg4_pool) and with cfg4_host_batch's layout: (b1 - b0, CFG4_STRIDE) uint8, zero-padded."""
+    k = b1 - b0
+    out = np.zeros((k, CFG4_STRIDE), np.uint8)
+    out[:, 4:12] = np.frombuffer(CFG4_TXS.to_bytes(8, "little"), np.uint8)
+    pos = 12 + np.arange(CFG4_TXS) * (8 + CFG4_TX_BYTES)
+    lenb = np.frombuffer(CFG4_TX_BYTES.to_bytes(8, "little"), np.uint8)
+    for j in range(8):
+        out[:, pos + j] = lenb[j]
+    out[:, pos + 8] = 1
+    ctr = np.arange(b0, b1, dtype=np.uint64)[:, None] * CFG4_TXS + np.arange(CFG4_TXS, dtype=np.uint64)[None, :]
+    be = ctr.astype(">u8").view(np.uint8).reshape(k, CFG4_TXS, 8)
+    for j in range(8):
+        out[:, pos + 9 + j] = be[:, :, j]
+    return out
+
+
+def check_cfg4_digests(data, outs, pool: int, nb: int, threads: int, chunk: int = 512):
+    """Every digest of the config-4 launch (nb ranges cycling a pool of `pool` batches, message i =
+    pool batch i mod pool): out[i] == out[i mod pool] for all i (on the device), and for every pool
+    batch its bytes equal the host construction (cfg4_pool_host) and its digest equals hashlib's
+    (OpenSSL) SHA-512[..32], hashed on `threads` host threads.  worker/src/processor.rs:38."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    idx = torch.arange(nb, device=outs.device, dtype=torch.int64) % pool
+    periodic = bool((outs == outs[idx]).all().item())
+    npool = min(pool, nb)
+    o = outs[:npool].cpu().numpy()
+    bad_bytes = bad_dig = 0
+    with ThreadPoolExecutor(threads) as ex:
+        for b0 in range(0, npool, chunk):
+            b1 = min(npool, b0 + chunk)
+            dev = data[b0 * CFG4_STRIDE:b1 * CFG4_STRIDE].view(b1 - b0, CFG4_STRIDE).cpu().numpy()
+            host = cfg4_pool_host(b0, b1)
+            bad_bytes += int((dev[:, :CFG4_BATCH_BYTES] != host[:, :CFG4_BATCH_BYTES]).any(axis=1).sum())
+            digs = list(ex.map(lambda r: hashlib.sha512(r[:CFG4_BATCH_BYTES]).digest()[:32], host))
+            bad_dig += sum(d != o[b0 + i].tobytes() for i, d in enumerate(digs))
+    ok = periodic and bad_bytes == 0 and bad_dig == 0
+    return ok, {"digests_checked": nb, "pool_batches_vs_hashlib": npool, "periodic": periodic,
+                "pool_bytes_mismatch": bad_bytes, "digest_mismatch": bad_dig}
+
+
 def bench_cfg1(lib, calls: int = 10000, cpu_baseline: bool = False):
     """BASELINE config 1 (SURVEY.md §8(d)): Signature::verify_batch on the reference's 4-node
     certificate -- the crypto_tests.rs fixture keys (ChaCha20-seeded, tests/golden), digest =
@@ -386,15 +429,12 @@ def cpu_baseline_cfg3(cdig, pks, sigs, m: int, Q: int, bad, budget_s: float):
                       "C restatement, %d threads, %.1f s)" % (k, th, dt)}
 
 
-def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
-    """BASELINE config 3: 100-node committee, m certificates x 67 votes (quorum 2N/3+1,
-    config/src/lib.rs:181-186), each vote invalid with p = 0.01 (signed over another digest).
-    Leaf equations for every vote + per-certificate AND; bad-vote sets checked against the
-    construction.  Timed without any key cache (the per-vote ladder; dalek's batch equation over
-    sub-batches), with the launch keys the library detects itself (no nwc_set_committee: first
-    launch incl. the census and the 100 keys' comb builds, then steady state), and with the
-    committee key cache."""
-    from narwhal_amd import _lib, device
+def make_cfg3(m: int, clean: bool = True):
+    """BASELINE config 3's certificates: a 100-node committee (seeds "nw-committee"),
+    m certificates (digests "nw-cert") x 67 distinct voters (seeded permutation, 0x4E57), each vote
+    invalid with p = 0.01 (signed over the digest with one bit flipped); with clean=True also the same
+    votes all valid.  Keys and signatures from the GPU signer; every tensor resident in HBM."""
+    from narwhal_amd import device
     import torch
     N, Q = 100, 67
     nv = m * Q
@@ -409,12 +449,46 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
     signed[bad, 0] ^= 1
     pks, sigs = device.keygen_sign(cseeds[voters], signed)
     offs = (torch.arange(m + 1, device="cuda", dtype=torch.int32) * Q)
-    committee_pks, _ = device.keygen_sign(cseeds, cdig[:N])
+    committee_pks, _ = device.keygen_sign(cseeds, torch.zeros((N, 32), dtype=torch.uint8, device="cuda"))
+    out = {"N": N, "Q": Q, "nv": nv, "m": m, "cdig": cdig, "msg_index": msg_index, "offs": offs, "pks": pks,
+           "sigs": sigs, "bad": bad, "committee_pks": committee_pks}
+    if clean:
+        # the same certificates with every vote valid (dalek's batch equation pays on clean traffic)
+        out["clean_pks"], out["clean_sigs"] = device.keygen_sign(cseeds[voters], cdig[msg_index.long()])
+        out["no_bad"] = torch.zeros_like(bad)
     torch.cuda.synchronize()
-    # the same certificates with every vote valid (dalek's batch equation pays on clean traffic)
-    clean_pks, clean_sigs = device.keygen_sign(cseeds[voters], cdig[msg_index.long()])
-    no_bad = torch.zeros_like(bad)
-    torch.cuda.synchronize()
+    return out
+
+
+def cert_shard(offs, world: int, rank: int):
+    """Certificates [c0, c1) of rank `rank`: whole certificates, balanced by votes -- the cut before
+    rank r is the first certificate boundary at or past r/world of the votes (nwc_cert_cuts)."""
+    offs = np.asarray(offs, dtype=np.int64)
+    m, nv = len(offs) - 1, int(offs[-1])
+
+    def cut(r):
+        if r <= 0:
+            return 0
+        if r >= world:
+            return m
+        return int(np.searchsorted(offs, nv * r // world, side="left"))
+    return cut(rank), cut(rank + 1)
+
+
+def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
+    """BASELINE config 3: 100-node committee, m certificates x 67 votes (quorum 2N/3+1,
+    config/src/lib.rs:181-186), each vote invalid with p = 0.01 (signed over another digest).
+    Leaf equations for every vote + per-certificate AND; bad-vote sets checked against the
+    construction.  Timed without any key cache (the per-vote ladder; dalek's batch equation over
+    sub-batches), with the launch keys the library detects itself (no nwc_set_committee: first
+    launch incl. the census and the 100 keys' comb builds, then steady state), and with the
+    committee key cache."""
+    from narwhal_amd import _lib
+    import torch
+    inst = make_cfg3(m)
+    N, Q, nv = inst["N"], inst["Q"], inst["nv"]
+    cdig, msg_index, offs, pks, sigs, bad = (inst[k] for k in ("cdig", "msg_index", "offs", "pks", "sigs", "bad"))
+    committee_pks, clean_pks, clean_sigs, no_bad = (inst[k] for k in ("committee_pks", "clean_pks", "clean_sigs", "no_bad"))
     out = {}
     legs = (("no_cache", False, "leaf", pks, sigs, bad), ("no_cache_straus", False, "straus", pks, sigs, bad),
             ("clean_no_cache", False, "leaf", clean_pks, clean_sigs, no_bad),
@@ -492,6 +566,82 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
     out["bad_votes"] = int(bad.sum().item())
     out["failing_certs"] = int(bad.view(m, Q).any(dim=1).sum().item())
     return out
+
+
+def bench_cfg3_sharded(lib, rank: int, world: int, m: int, steps: int):
+    """Config 3 at world > 1: whole certificates sharded over the ranks, balanced by
+    votes (cert_shard = nwc_cert_cuts), no data-path collective.  Every rank builds the same
+    instance (seeded), keeps its certificates' votes resident in its GPU's HBM and runs the
+    production batch-leaf path (launch keys detected by the library: the first call includes the
+    census and the comb builds, then `steps` timed calls); value = all ranks' votes / the slowest
+    rank's time.  The certificate and bad-vote words are then all-gathered over the process group
+    (timed separately; not needed for correctness: each rank holds its own verdicts) and rank 0
+    checks the whole set against the construction."""
+    from narwhal_amd import _lib, device
+    import torch
+    import torch.distributed as dist
+    inst = make_cfg3(m, clean=False)
+    Q, nv = inst["Q"], inst["nv"]
+    c0, c1 = cert_shard(inst["offs"].cpu().numpy(), world, rank)
+    v0, v1 = c0 * Q, c1 * Q
+    mc, nvl = c1 - c0, v1 - v0
+    cdig = inst["cdig"][c0:c1].contiguous()
+    pks, sigs = inst["pks"][v0:v1].contiguous(), inst["sigs"][v0:v1].contiguous()
+    offs = (inst["offs"][c0:c1 + 1] - v0).contiguous()
+    msg_index = (inst["msg_index"][v0:v1] - c0).contiguous()
+    bad = inst["bad"]
+    del inst
+    _lib.check(lib.nwc_set_committee(None, 0))
+    _lib.diag_set("launch_keys", 1)
+    words = torch.empty(device.words_for(max(nvl, 1)), dtype=torch.int64, device="cuda")
+    run = lambda: device.cert_reduce(device.verify(cdig, pks, sigs, strict=False, msg_index=msg_index,  # noqa: E731
+                                                   out=words), offs, nvl)
+    barrier(world)
+    t0 = time.perf_counter()
+    run()
+    barrier(world)
+    first_ms = max_over_ranks((time.perf_counter() - t0) * 1e3, world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        cw, bw = run()
+    barrier(world)
+    dt = max_over_ranks((time.perf_counter() - t0) / steps, world)
+    # gather: per rank its certificate words and bad-vote words, padded to the largest shard
+    cmax = max(cert_shard(np.arange(m + 1) * Q, world, r)[1] - cert_shard(np.arange(m + 1) * Q, world, r)[0]
+               for r in range(world))
+    cwords, vwords = device.words_for(cmax), device.words_for(cmax * Q)
+    pc = torch.zeros(cwords, dtype=torch.int64, device="cuda")
+    pv = torch.zeros(vwords, dtype=torch.int64, device="cuda")
+    pc[:cw.numel()] = cw
+    pv[:bw.numel()] = bw
+    allc = torch.empty(world * cwords, dtype=torch.int64, device="cuda")
+    allv = torch.empty(world * vwords, dtype=torch.int64, device="cuda")
+    barrier(world)
+    tg = time.perf_counter()
+    dist.all_gather_into_tensor(allc, pc)
+    dist.all_gather_into_tensor(allv, pv)
+    barrier(world)
+    gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, world)
+    ok = True
+    if rank == 0:
+        got_cert, got_bad = [], []
+        for r in range(world):
+            r0, r1 = cert_shard(np.arange(m + 1) * Q, world, r)
+            got_cert.append(device.unpack_bits(allc[r * cwords:(r + 1) * cwords], r1 - r0))
+            got_bad.append(device.unpack_bits(allv[r * vwords:(r + 1) * vwords], (r1 - r0) * Q))
+        want_bad = bad.cpu().numpy()
+        ok = bool((np.concatenate(got_bad) == want_bad).all() and
+                  (np.concatenate(got_cert) == ~want_bad.reshape(m, Q).any(axis=1)).all())
+    okt = torch.tensor([1 if ok else 0], dtype=torch.int64, device="cuda")
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    h = ctypes.c_uint32()
+    _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
+    return {"workload": "cfg3: %d certificates x %d votes, 1%% invalid, whole certificates sharded %d ways (balanced by "
+                        "votes), launch keys, certificate AND + bad-vote set" % (m, Q, world),
+            "launch_keys": {"votes_per_s": nv / dt, "certs_per_s": m / dt, "ms_per_step": dt * 1e3,
+                            "first_call_ms": first_ms, "launch_keys_held": h.value},
+            "votes_per_gpu": nvl, "scaling": "strong", "verdict_allgather_ms": gather_ms,
+            "allgather_needed": False, "parity_ok": bool(okt.item() == 1)}
 
 
 def bench_cfg3_host_abi(lib, cdig, offs, pks, sigs, bad, m: int, Q: int, reps: int = 3):
@@ -825,47 +975,55 @@ def openssl_version():
     return ssl.OPENSSL_VERSION.split()[1] if ssl.OPENSSL_VERSION.startswith("OpenSSL") else ssl.OPENSSL_VERSION
 
 
-def cpu_baseline_digest(budget_s: float):
+def cpu_baseline_digest(budget_s: float, data, outs):
+    """The C restatement's SHA-512 (oracle/, "port") on the host cores over the first 4 x threads
+    batches of the GPU leg's own pool (copied from HBM), every CPU digest compared byte for byte
+    with the GPU's digest of the same batch."""
     from tests.oracle_lib import load_oracle
     orc = load_oracle()
     th = cpu_threads()
     nb = 4 * th
-    blob = b"".join(cfg4_host_batch(b) for b in range(nb))
-    data = np.frombuffer(blob, dtype=np.uint8)
+    rows = data[:nb * CFG4_STRIDE].view(nb, CFG4_STRIDE)[:, :CFG4_BATCH_BYTES].cpu().numpy()
+    host = np.ascontiguousarray(rows).reshape(-1)
     offs = np.arange(nb + 1, dtype=np.uint64) * CFG4_BATCH_BYTES
+    gpu = outs[:nb].cpu().numpy()
     t0 = time.perf_counter()
     reps = 0
     while True:
-        orc.digest_many(data, offs, th)
+        got = orc.digest_many(host, offs, th)
         reps += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    out = {"value": reps * len(blob) / dt / 1e9, "unit": "GB/s", "cores": th, "kind": "port",
-           "value_per_thread": reps * len(blob) / dt / 1e9 / th,
-           "sample": "%d x %d cfg-4 batches (C restatement SHA-512, %d threads, %.1f s)" % (reps, nb, th, dt)}
-    out["openssl"] = cpu_digest_openssl(blob, nb, th, budget_s / 2)
+    out = {"value": reps * host.size / dt / 1e9, "unit": "GB/s", "cores": th, "kind": "port",
+           "value_per_thread": reps * host.size / dt / 1e9 / th,
+           "parity_ok": bool((np.asarray(got).reshape(nb, 32) == gpu).all()),
+           "sample": "%d x %d cfg-4 batches of the GPU leg's pool (C restatement SHA-512, %d threads, %.1f s); "
+                     "every digest compared with the GPU's" % (reps, nb, th, dt)}
+    out["openssl"] = cpu_digest_openssl(host, nb, th, budget_s / 2, gpu)
     return out
 
 
-def cpu_digest_openssl(blob: bytes, nb: int, th: int, budget_s: float):
+def cpu_digest_openssl(blob: np.ndarray, nb: int, th: int, budget_s: float, gpu: np.ndarray):
     """SURVEY.md §8(d)'s digest baseline: OpenSSL SHA-512 (hashlib, which releases the GIL on
-    large inputs) over the same cfg-4 batches on `th` host threads, one batch per call."""
+    large inputs) over the same cfg-4 batches on `th` host threads, one batch per call; its digests
+    compared with the GPU's."""
     from concurrent.futures import ThreadPoolExecutor
     mv = memoryview(blob)
     views = [mv[b * CFG4_BATCH_BYTES:(b + 1) * CFG4_BATCH_BYTES] for b in range(nb)]
-    ok = hashlib.sha512(views[0]).digest()[:32] == hashlib.sha512(cfg4_host_batch(0)).digest()[:32]
     with ThreadPoolExecutor(th) as ex:
         t0 = time.perf_counter()
         reps = 0
         while True:
-            list(ex.map(lambda v: hashlib.sha512(v).digest()[:32], views))
+            got = list(ex.map(lambda v: hashlib.sha512(v).digest()[:32], views))
             reps += 1
             if time.perf_counter() - t0 > budget_s:
                 break
         dt = time.perf_counter() - t0
+    ok = all(g == gpu[b].tobytes() for b, g in enumerate(got))
     return {"value": reps * nb * CFG4_BATCH_BYTES / dt / 1e9, "unit": "GB/s", "cores": th, "kind": "openssl",
-            "parity_ok": ok, "sample": "%d x %d cfg-4 batches (hashlib/OpenSSL SHA-512, %d threads, %.1f s)" % (reps, nb, th, dt)}
+            "parity_ok": ok, "sample": "%d x %d cfg-4 batches (hashlib/OpenSSL SHA-512, %d threads, %.1f s); every "
+                                       "digest compared with the GPU's" % (reps, nb, th, dt)}
 
 
 def roofline_verify(vpc, n: int, kernel_ms: float, effective_tops: float, clock=None):
@@ -1069,6 +1227,18 @@ def main():
         clock = {"clock_ghz": ghz, "waves": waves, "after_launches": reps,
                  "ok": bool(device.unpack_bits(words, n).all())}
 
+    # reject side of the headline leg (outside the timed region): the same triples with 1 in 64
+    # signatures corrupted (one bit of byte (i / 64) mod 64: R or s), verdicts equal to the construction
+    bad_sigs = sigs.clone()
+    ci = torch.arange(0, n, 64, device="cuda")
+    bad_sigs[ci, (ci // 64) % 64] ^= 0x10
+    rwords = torch.empty_like(words)
+    device.verify(msgs, pks, bad_sigs, strict=True, out=rwords)
+    want = np.ones(n, dtype=bool)
+    want[::64] = False
+    reject = {"corrupted": int(ci.numel()), "verdicts_ok": bool((device.unpack_bits(rwords, n) == want).all())}
+    del bad_sigs, rwords
+
     # ---------------- digest leg (cfg 4)
     digest = None
     if args.digest_batches > 0:
@@ -1094,15 +1264,16 @@ def main():
         ddt = max_over_ranks(time.perf_counter() - t0, world)
         dk_ms = sum(e0.elapsed_time(e1) for e0, e1 in devs) / len(devs)
         dbytes = world * nb * CFG4_BATCH_BYTES * args.digest_steps
-        o = outs[:3].cpu().numpy()
-        dok = all(o[b].tobytes() == hashlib.sha512(cfg4_host_batch(b)).digest()[:32] for b in range(3))
+        # every one of the nb digests (outside the timed region): periodicity over the pool on the
+        # device, the pool's bytes and digests against an independent host construction + hashlib
+        dok, dcheck = check_cfg4_digests(data, outs, pool, nb, cpu_threads())
         dk_gbs = nb * CFG4_BATCH_BYTES / (dk_ms * 1e-3) / 1e9
         # launch_digest's choice: McNaughton-scheduled blocks above one wave per SIMD of messages
         cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
         dkernel = "k_sha512_digest32_sched" if nb > 64 * 4 * cus else "k_sha512_digest32"
         digest = {"metric": "batch digest GB/s", "value": dbytes / ddt / 1e9, "unit": "GB/s",
                   "batches": nb, "batch_bytes": CFG4_BATCH_BYTES, "pool_distinct_batches": pool,
-                  "parity_ok": dok, "kernel": dkernel, "kernel_ms": dk_ms, "kernel_GBps": dk_gbs,
+                  "parity_ok": dok, "parity": dcheck, "kernel": dkernel, "kernel_ms": dk_ms, "kernel_GBps": dk_gbs,
                   "hbm_frac": dk_gbs / HBM_PEAK_GBS,
                   "effective_valu_frac": dk_gbs * 1e9 / 128 * OPS_SHA / (VALU_PEAK_TOPS * 1e12)}
 
@@ -1120,6 +1291,8 @@ def main():
     if world == 1 and args.cfg3_certs > 0:
         extras["cfg3"] = bench_cfg3(lib, args.cfg3_certs, max(1, args.steps // 2),
                                     args.cpu_budget / 2 if rank == 0 else 0.0)
+    elif args.cfg3_certs > 0:
+        extras["cfg3"] = bench_cfg3_sharded(lib, rank, world, args.cfg3_certs, max(1, args.steps // 2))
     if world == 1 and args.cfg1_calls > 0:
         extras["cfg1"] = bench_cfg1(lib, args.cfg1_calls, cpu_baseline=args.cpu_budget > 0)
     if world == 1 and args.wire_certs > 0:
@@ -1130,7 +1303,7 @@ def main():
         progress("CPU baselines")
         cpu = cpu_baseline_verify(msgs, pks, sigs, args.cpu_budget)
         if digest is not None:
-            digest["cpu_baseline"] = cpu_baseline_digest(args.cpu_budget / 2)
+            digest["cpu_baseline"] = cpu_baseline_digest(args.cpu_budget / 2, data, outs)
 
     vpc = profile_counters("nwc::k_verify<true, false, false, false>", "nwc::k_verify<true, false, false>",
                            "nwc::k_verify<true, false>")
@@ -1153,7 +1326,7 @@ def main():
             "config": {"workload": "cfg2: %d independent (32-B msg, pk, sig) triples per GPU, all valid, "
                                    "verify_strict" % n,
                        "global_batch": world * n, "parallelism": "shard%d" % world,
-                       "verdicts_ok": ok, "verdict_allgather_ms": gather_ms,
+                       "verdicts_ok": ok, "reject_check": reject, "verdict_allgather_ms": gather_ms,
                        "allgather_needed": False},
             "roofline": roofline_verify(vpc, n, kernel_ms, effective_tops, clock),
             "cpu_baseline": cpu,

@@ -82,7 +82,9 @@ int nwc_diag_set(const char* name, int64_t value);
  * Every wave stamps s_memtime / s_memrealtime at entry and exit; *clock_ghz = the median over
  * waves of delta(memtime) / delta(realtime) x 100 MHz, *waves = the waves counted.  Call it after
  * some seconds of back-to-back launches (MI355X_MICROARCH.md, DVFS item 6).  The verdict words
- * are written as by nwc_dev_verify.  Diagnostics only, not part of the crate's API. */
+ * are written as by nwc_dev_verify.  NWC_ERR_ARG with a committee cache set (strict launches would
+ * take the comb kernel, which has no stamps) or n > NWC_VERIFY_MAX_LAUNCH (a split launch).
+ * Diagnostics only, not part of the crate's API. */
 int nwc_diag_verify_clock(const void* d_msgs, uint64_t msg_stride, const void* d_pks, const void* d_sigs, uint64_t n,
                           void* d_verdict_words, void* stream, double* clock_ghz, uint32_t* waves);
 

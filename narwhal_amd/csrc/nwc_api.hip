@@ -2018,6 +2018,11 @@ int nwc_diag_verify_clock(const void* d_msgs, uint64_t msg_stride, const void* d
   DEV_PROLOGUE
   if (!d_msgs || !d_pks || !d_sigs || !d_verdict_words || !clock_ghz) return set_err(NWC_ERR_ARG, "null buffer");
   if (n < 4096) return set_err(NWC_ERR_ARG, "the clock stamp needs a full launch (n >= 4096)");
+  // the stamps come from the plain k_verify launch: a committee cache would send these strict
+  // equations to the comb kernel (no stamps), and a split launch would overwrite them
+  if (d.cm_n) return set_err(NWC_ERR_ARG, "the clock stamp needs the plain k_verify path: clear the committee cache first");
+  if (n > verify_max_launch())
+    return set_err(NWC_ERR_ARG, "the clock stamp needs a single launch (n <= %llu)", (unsigned long long)verify_max_launch());
   // one stamp slot per wave of the largest grid launch_verify gives k_verify
   const uint64_t nwaves = (uint64_t)d.cus * d.verify_blocks_per_cu * NWC_VERIFY_GRID_MULT * 4;
   if (!d.stamps) HIP_TRY(hipMalloc(&d.stamps, 32 * nwaves));
