@@ -495,14 +495,16 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
             ("clean_no_cache_straus", False, "straus", clean_pks, clean_sigs, no_bad),
             ("no_cache_msm", False, "msm", pks, sigs, bad),
             ("clean_no_cache_msm", False, "msm", clean_pks, clean_sigs, no_bad),
-            ("launch_keys", False, "launch", pks, sigs, bad), ("cache", True, "leaf", pks, sigs, bad))
+            ("launch_keys", False, "launch", pks, sigs, bad), ("cache", True, "leaf", pks, sigs, bad),
+            ("dalek_launch_keys", False, "dalek", pks, sigs, bad),
+            ("clean_dalek_launch_keys", False, "dalek", clean_pks, clean_sigs, no_bad))
     only = os.environ.get("NWC_BENCH_CFG3_LEGS")   # profiling: a comma-separated subset of the legs
     for tag, use_cache, eq, P, S, want_bad in legs:
         if only and tag not in only.split(","):
             continue
         progress("config 3: " + tag)
         _lib.check(lib.nwc_set_committee(None, 0))   # no committee cache, launch keys emptied
-        _lib.diag_set("launch_keys", 1 if eq == "launch" else 0)
+        _lib.diag_set("launch_keys", 1 if eq in ("launch", "dalek") else 0)
         if use_cache:
             cpk = committee_pks.cpu().numpy()
             _lib.check(lib.nwc_set_committee(_lib.buf(cpk), N))
@@ -510,7 +512,9 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
         if eq == "straus":
             run = lambda: device.cert_reduce(device.verify_batch_straus(cdig, offs, msg_index, P, S, out=words),  # noqa
                                              offs, nv)
-        elif eq == "msm":
+        elif eq in ("msm", "dalek"):
+            # the same entry: launch keys off -> Pippenger groups first; on -> comb leaves + dalek's
+            # equation per certificate over the failing votes (resolve.h)
             run = lambda: device.cert_reduce(device.verify_batch_msm(cdig, offs, msg_index, P, S, out=words),  # noqa
                                              offs, nv)
             st0 = device.msm_stats()
@@ -545,14 +549,17 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
                                         "aggregated, wavefront-level bucket reduction), Straus sub-batches for failing groups, "
                                         "leaves for failing sub-batches; device-side skip policy while most groups fail",
                                  "launch": "per-vote leaves; the launch's repeated keys detected by the library (no nwc_set_committee), "
-                                           "their combs built on the first call, comb kernel from then on"}.get(eq, "per-vote leaves"),
+                                           "their combs built on the first call, comb kernel from then on",
+                                 "dalek": "dalek's batch semantics (nwc_dev_verify_batch_msm with launch keys): comb leaves for every vote, "
+                                          "then dalek's equation once per certificate over the votes they reject, in E[8] (resolve.h)"
+                                 }.get(eq, "per-vote leaves"),
                     "bad_rate": 0.01 if want_bad is bad else 0.0}
-        if eq == "msm":
+        if eq in ("msm", "dalek"):
             st1 = device.msm_stats()
             out[tag]["msm_groups"] = {"passed": st1[0] - st0[0], "failed": st1[1] - st0[1],
                                       "key_overflow": st1[2] - st0[2], "skipped": st1[3] - st0[3],
                                       "calls": nsteps + 1}
-        if eq == "launch":
+        if eq in ("launch", "dalek"):
             h = ctypes.c_uint32()
             _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
             out[tag]["launch_keys_held"] = h.value

@@ -2304,6 +2304,7 @@ __global__ __launch_bounds__(256) void k_keygen_sign(const uint8_t* __restrict__
 }  // namespace nwc
 #include "straus.h"
 #include "msm.h"
+#include "resolve.h"
 namespace nwc {
 
 // Seeds / messages of the synthetic workloads (SURVEY.md §8(d) cfg 2):

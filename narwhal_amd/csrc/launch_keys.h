@@ -22,7 +22,7 @@
 
 namespace nwc {
 
-constexpr u32 LK_MAX_KEYS = 128;       // keys held (20 MB of radix-2^14 comb each: 2.6 GB)
+constexpr u32 LK_MAX_KEYS = 128;       // keys held at most (20 MB of radix-2^14 comb each; allocated as keys join)
 constexpr u32 LK_SLOTS = 1024;         // committee_lookup table of the held keys (load <= 1/8)
 constexpr u32 LK_SAMPLES = 16384;      // equations sampled per launch
 constexpr u32 LK_CENSUS = 8192;        // LDS census slots (power of two)
@@ -34,9 +34,11 @@ struct LaunchKeys {
   u32* keys;            // LK_MAX_KEYS x 8 words
   u32* flags;           // KEY_DECODES | KEY_SMALL_ORDER | KEY_TORSION
   int32_t* slots;       // LK_SLOTS, -1 = empty
-  ge_niels_pad* comb;   // LK_MAX_KEYS x COMB_PER_KEY
+  ge_niels_pad* comb;   // cap x COMB_PER_KEY (grown by the host as keys ask to join)
   ge_p3* bases;         // LK_MAX_KEYS x KeyComb::windows
-  u32* state;           // [0] keys held, [1] keys held before this launch's select
+  u32* state;           // [0] keys held, [1] keys held before this launch's select, [2] keys it would hold
+  u32* host_demand;     // host-mapped copy of state[2] (the host grows `comb` from it without a sync)
+  u32 cap;              // keys `comb` has room for: joins stop there
 };
 
 __device__ __forceinline__ bool key_equal(const uint8_t* pks, u32 idx, const u32 aw[8]) {
@@ -111,7 +113,12 @@ __global__ __launch_bounds__(1024) void k_lk_select(const uint8_t* pks, uint64_t
   }
   if (threadIdx.x == 0) {
     const u32 held = reset ? 0u : held0;
-    const u32 add = min(nfresh, LK_MAX_KEYS - held);
+    // the keys that want to join and fit the policy's limit; those beyond the comb's allocated room
+    // wait for the host to grow it (their votes take the ladder meanwhile)
+    const u32 demand = min(held + nfresh, LK_MAX_KEYS);
+    lk.state[2] = demand;
+    if (lk.host_demand) *reinterpret_cast<volatile u32*>(lk.host_demand) = demand;
+    const u32 add = min(nfresh, (lk.cap > held ? lk.cap : held) - held);
     u32 q = held;
     for (u32 k = 0; k < add; ++k) {
       u32 aw[8];

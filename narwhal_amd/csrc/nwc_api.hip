@@ -132,9 +132,12 @@ struct DevCtx {
   uint8_t* msm_scratch = nullptr;      // k_verify_msm per-wave points and digits (nwc_dev_verify_batch_msm)
   size_t msm_cap = 0;
   uint32_t* msm_stats = nullptr;       // groups passed / failed / key overflow (nwc_msm_stats)
+  uint8_t* rs_buf = nullptr;           // dalek's equation per certificate (resolve.h): failing-vote list, certificate states
+  size_t rs_cap = 0;
   uint32_t* uc_list = nullptr;     // k_verify_comb: equations whose key is not cached
   uint32_t* uc_count = nullptr;
   bool hold_lists = false;         // a call with a deferred list pending: ensure_scratch does not shrink the lists
+  bool tables_ready = false;       // ensure_verify_tables has built the basepoint tables, memo and auto cache
   // k_verify per-lane table slots; reused by every launch, so launches that use it are
   // serialised across streams with `scratch_free` (recorded after each such launch).
   uint8_t* scratch = nullptr;
@@ -193,6 +196,8 @@ struct DevCtx {
   // launch keys (launch_keys.h): allocated by the first large batch-leaf launch without a committee
   nwc::LaunchKeys lk{};
   bool lk_alloc = false;
+  bool lk_censused = false;           // the first launch-key launch has measured its keys' demand
+  uint32_t* lk_demand = nullptr;      // host-mapped demand word (lk.host_demand's host side)
   // large host calls: pageable inputs through pinned stages on `xfer` (created on first use)
   std::unique_ptr<HostStager> stager;
   std::mutex mu;
@@ -291,6 +296,7 @@ struct Knobs {
   std::atomic<uint32_t> launch_keys{1};   // NWC_LAUNCH_KEYS: 0 = large batch-leaf launches never build launch keys
   std::atomic<uint32_t> msm_group{0};     // NWC_MSM_GROUP: votes per Pippenger group of k_verify_msm (0 = sized per launch)
   std::atomic<uint32_t> msm_adapt{1};     // NWC_MSM_ADAPT: 0 = the equation on every group (no skip policy)
+  std::atomic<uint64_t> dalek_seed{0};    // tests: fixed seed of the per-certificate equation's z_i (0 = host CSPRNG)
   Knobs() {
     if (const char* e = std::getenv("NWC_LAUNCH_KEYS")) launch_keys = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("NWC_STRAUS_NQ")) straus_nq = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -326,6 +332,17 @@ int init_device(DevCtx& d) {
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(nwc::k_verify_comb), 256, 0));
   d.comb_blocks_per_cu = bpc > 0 ? bpc : 1;
   HIP_TRY(hipMalloc(&d.uc_count, sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  return 0;
+}
+
+// The verification tables, built by the first call that verifies (or signs) on the device, not at
+// nwc_init: a worker process that only digests batches holds none of them (worker/src/worker.rs:
+// 182-188 -- workers and a primary share the host's GPUs).  Built on d.stream and waited for once,
+// so launches on any stream after it see them.  Caller holds d.mu and has set the device.
+int ensure_verify_tables(DevCtx& d) {
+  if (d.tables_ready) return 0;
   HIP_TRY(hipMalloc(&d.comb_base, nwc::BaseComb::per * sizeof(nwc::ge_niels_pad)));
   hipLaunchKernelGGL(nwc::k_build_comb<nwc::BaseComb>, dim3((unsigned)((nwc::BaseComb::per + 255) / 256)), dim3(256), 0, d.stream,
                      (const nwc::u32*)nullptr, 1u, d.comb_base);
@@ -341,7 +358,6 @@ int init_device(DevCtx& d) {
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipMalloc(&d.base_table, 2 * 129 * sizeof(nwc::ge_niels)));
-  HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
   hipLaunchKernelGGL(nwc::k_build_base_table, dim3(5), dim3(64), 0, d.stream, d.base_table);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMalloc(&d.base24, 2 * (size_t)nwc::B24_ENTRIES * sizeof(nwc::ge_niels_pad)));
@@ -363,10 +379,13 @@ int init_device(DevCtx& d) {
     d.ak_slot_cap = 64;
     while (d.ak_slot_cap < 8 * std::min<uint32_t>(acap, 16u)) d.ak_slot_cap <<= 1;
     HIP_TRY(hipMalloc(&d.ak_slots, 4 * (size_t)d.ak_slot_cap));
-    d.kb_cap = 64 * (size_t)nwc::KeyComb::windows;
-    HIP_TRY(hipMalloc(&d.kb_bases, d.kb_cap * sizeof(nwc::ge_p3)));
+    if (!d.kb_bases) {
+      d.kb_cap = 64 * (size_t)nwc::KeyComb::windows;
+      HIP_TRY(hipMalloc(&d.kb_bases, d.kb_cap * sizeof(nwc::ge_p3)));
+    }
   }
   HIP_TRY(hipStreamSynchronize(d.stream));
+  d.tables_ready = true;
   return 0;
 }
 
@@ -687,20 +706,58 @@ uint64_t cold_max() {
   return m;
 }
 
-// Device buffers of the launch keys (launch_keys.h), allocated once per device; the set starts
-// empty.  Caller holds d.mu.
+// Device buffers of the launch keys (launch_keys.h), allocated once per device except the combs
+// (20 MB per key), which grow as keys ask to join; the set starts empty.  Caller holds d.mu.
 int lk_ensure(DevCtx& d, hipStream_t s) {
   if (d.lk_alloc) return 0;
   nwc::LaunchKeys& k = d.lk;
   HIP_TRY(hipMalloc(&k.keys, 32 * (size_t)nwc::LK_MAX_KEYS));
   HIP_TRY(hipMalloc(&k.flags, 4 * (size_t)nwc::LK_MAX_KEYS));
   HIP_TRY(hipMalloc(&k.slots, 4 * (size_t)nwc::LK_SLOTS));
-  HIP_TRY(hipMalloc(&k.comb, (size_t)nwc::LK_MAX_KEYS * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad)));
   HIP_TRY(hipMalloc(&k.bases, (size_t)nwc::LK_MAX_KEYS * nwc::KeyComb::windows * sizeof(nwc::ge_p3)));
   HIP_TRY(hipMalloc(&k.state, 16));
+  if (!d.lk_demand) {
+    HIP_TRY(hipHostMalloc(&d.lk_demand, sizeof(uint32_t), hipHostMallocCoherent));
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, d.lk_demand, 0));
+    k.host_demand = static_cast<uint32_t*>(dp);
+  }
+  *reinterpret_cast<volatile uint32_t*>(d.lk_demand) = 0;
+  k.comb = nullptr;
+  k.cap = 0;
   HIP_TRY(hipMemsetAsync(k.slots, 0xFF, 4 * (size_t)nwc::LK_SLOTS, s));
   HIP_TRY(hipMemsetAsync(k.state, 0, 16, s));
   d.lk_alloc = true;
+  d.lk_censused = false;
+  return 0;
+}
+
+// Room for the keys that asked to join: the first launch-key launch runs the census once and waits
+// for its demand; later launches read the demand the previous ones left in host memory (no sync)
+// and grow the combs stream-ordered on s (held combs copied), so a key that did not fit joins at
+// the next launch.  Called after s waits for scratch_free (no launch still reads the set).
+int lk_reserve(DevCtx& d, const uint8_t* pks, uint64_t n, hipStream_t s) {
+  nwc::LaunchKeys& k = d.lk;
+  if (k.cap >= nwc::LK_MAX_KEYS) return 0;
+  if (!d.lk_censused) {
+    // cap 0 and nothing held: the select only counts (no key joins), then the host reads its demand
+    hipLaunchKernelGGL(nwc::k_lk_select, dim3(1), dim3(1024), 0, s, pks, n, k);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    d.lk_censused = true;
+  }
+  const uint32_t demand = *reinterpret_cast<volatile uint32_t*>(d.lk_demand);
+  if (demand <= k.cap) return 0;
+  const uint32_t cap = std::min<uint32_t>(nwc::LK_MAX_KEYS, (demand + 7) / 8 * 8);
+  nwc::ge_niels_pad* comb = nullptr;
+  const size_t per = nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad);
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&comb), (size_t)cap * per, s));
+  if (k.comb) {
+    HIP_TRY(hipMemcpyAsync(comb, k.comb, (size_t)k.cap * per, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipFreeAsync(k.comb, s));
+  }
+  k.comb = comb;
+  k.cap = cap;
   return 0;
 }
 
@@ -741,6 +798,28 @@ int ensure_stager(DevCtx& d) {
   return 0;
 }
 
+// The batch entries' buffers (Straus tables, MSM groups, the per-certificate resolution) above
+// NWC_VERIFY_KEEP_BYTES that the current launch does not use are freed -- after every launch that
+// used them, each of which records scratch_free -- so a process that ran the Straus or MSM entry
+// once holds at most the keep threshold of them while it verifies by other paths.
+int release_idle_buffers(DevCtx& d, const uint8_t* in_use) {
+  const size_t keep = verify_keep_bytes();
+  struct Buf { uint8_t** p; size_t* cap; } bufs[] = {
+      {&d.straus_scratch, &d.straus_cap}, {&d.msm_scratch, &d.msm_cap}, {&d.rs_buf, &d.rs_cap}};
+  bool any = false;
+  for (const Buf& b : bufs) any = any || (*b.p && *b.p != in_use && *b.cap > keep);
+  if (!any) return 0;
+  HIP_TRY(hipEventSynchronize(d.scratch_free));
+  for (const Buf& b : bufs) {
+    if (*b.p && *b.p != in_use && *b.cap > keep) {
+      HIP_TRY(hipFree(*b.p));
+      *b.p = nullptr;
+      *b.cap = 0;
+    }
+  }
+  return 0;
+}
+
 // launch_verify flags: the caller checked on the host that every key is in the committee cache,
 // and/or out_words is already zero (both let the latency path run as a single kernel)
 // LV_AUTO: the keys are in the auto cache; LV_STAMP: the headline kernel's clock-stamp build
@@ -770,6 +849,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
                   hipStream_t s, int flags = 0, uint8_t* vbytes = nullptr, uint64_t list_base = 0) {
   if (n == 0) return 0;
+  if (int rc = ensure_verify_tables(d)) return rc;
+  if (int rc = release_idle_buffers(d, nullptr)) return rc;
   if (n > verify_max_launch() && !vbytes) {
     // consecutive launches of at most NWC_VERIFY_MAX_LAUNCH equations (a multiple of 64: whole
     // verdict words), so the per-launch lists stay bounded; every equation is independent, so the
@@ -856,6 +937,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   if (lk) {
     // the set's update is ordered after every launch that read it (scratch_free) and before this
     // launch's comb kernel; the builds exit at once when no key joined
+    if (int rc = lk_reserve(d, pks, n, s)) return rc;
     hipLaunchKernelGGL(nwc::k_lk_select, dim3(1), dim3(1024), 0, s, pks, n, d.lk);
     hipLaunchKernelGGL(nwc::k_lk_keys, dim3((nwc::LK_MAX_KEYS + 63) / 64), dim3(64), 0, s, d.lk);
     hipLaunchKernelGGL(nwc::k_build_comb_from_bases<nwc::KeyComb>, dim3((unsigned)(d.cus * 8)), dim3(256), 0, s,
@@ -1293,15 +1375,39 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
   return 0;
 }
 
-int ensure_straus_scratch(DevCtx& d, size_t bytes, hipStream_t s) {
-  if (bytes <= d.straus_cap) return 0;
+// A per-launch device buffer of the batch entries (MSM, Straus, resolve), grown on demand and
+// shrunk back when it holds more than NWC_VERIFY_KEEP_BYTES and a launch needs under a quarter of
+// it (a primary and workers share the GPU: worker/src/worker.rs:182,227).  Every launch that uses
+// these buffers records scratch_free after its last kernel, so waiting for it (and for s) drains
+// their users on any stream before the buffer is replaced.
+int ensure_buf(DevCtx& d, uint8_t*& p, size_t& cap, size_t need, hipStream_t s) {
+  const bool shrink = cap > verify_keep_bytes() && need < cap / 4;
+  if (need <= cap && !shrink) return 0;
+  HIP_TRY(hipEventSynchronize(d.scratch_free));
   HIP_TRY(hipStreamSynchronize(s));
-  if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
-  d.straus_scratch = nullptr;
-  d.straus_cap = 0;
-  HIP_TRY(hipMalloc(&d.straus_scratch, bytes));
-  d.straus_cap = bytes;
+  if (p) HIP_TRY(hipFree(p));
+  p = nullptr;
+  cap = 0;
+  HIP_TRY(hipMalloc(&p, need));
+  cap = need;
   return 0;
+}
+
+// The per-launch z_i seed: 32 bytes from the host's CSPRNG (dalek: merlin transcript + thread_rng),
+// or the test knob's fixed value (nwc_diag_set("dalek_seed")).
+void draw_seed(uint32_t seed[8]) {
+  const uint64_t fixed = knobs().dalek_seed.load();
+  if (fixed) {
+    for (int i = 0; i < 8; ++i) seed[i] = i == 0 ? (uint32_t)fixed : 0u;
+    return;
+  }
+  static thread_local std::random_device rd;
+  for (int i = 0; i < 8; ++i) seed[i] = rd();
+}
+
+int ensure_straus_scratch(DevCtx& d, size_t bytes, hipStream_t s) {
+  if (int rc = release_idle_buffers(d, d.straus_scratch)) return rc;
+  return ensure_buf(d, d.straus_scratch, d.straus_cap, bytes, s);
 }
 
 // dalek's batch equation over sub-batches (k_verify_straus) + the exact leaves for the failing
@@ -1310,6 +1416,7 @@ int ensure_straus_scratch(DevCtx& d, size_t bytes, hipStream_t s) {
 int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8_t* pks, const uint8_t* sigs,
                   uint64_t nvotes, uint64_t* leaf, hipStream_t s) {
   if (nvotes == 0) return 0;
+  if (int rc = ensure_verify_tables(d)) return rc;
   if (nvotes > verify_max_launch()) {
     // consecutive launches of at most NWC_VERIFY_MAX_LAUNCH votes, as launch_verify: sub-batches
     // are any consecutive votes (each reads its own certificate's digest through mi)
@@ -1335,11 +1442,7 @@ int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8
   HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
   nwc::StrausArgs sa{};
   sa.digests = dig; sa.msg_index = mi; sa.pks = pks; sa.sigs = sigs; sa.nv = nvotes; sa.runs = runs;
-  {
-    // 32 bytes from the host's CSPRNG per launch (dalek: merlin transcript + thread_rng)
-    static thread_local std::random_device rd;
-    for (int i = 0; i < 8; ++i) sa.seed[i] = rd();
-  }
+  draw_seed(sa.seed);
   sa.comb16 = d.comb16; sa.scratch = d.straus_scratch; sa.lane_stride = stride;
   sa.leaf_words = leaf; sa.list = d.uc_list; sa.count = d.uc_count;
   HIP_TRY(hipMemsetAsync(leaf, 0, 8 * ((nvotes + 63) / 64), s));
@@ -1367,6 +1470,7 @@ int launch_straus(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8
 int launch_msm(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8_t* pks, const uint8_t* sigs,
                uint64_t nvotes, uint64_t* leaf, hipStream_t s) {
   if (nvotes == 0) return 0;
+  if (int rc = ensure_verify_tables(d)) return rc;
   if (nvotes > verify_max_launch()) {
     const uint64_t step = verify_max_launch();
     for (uint64_t lo = 0; lo < nvotes; lo += step)
@@ -1396,66 +1500,100 @@ int launch_msm(DevCtx& d, const uint8_t* dig, const uint32_t* mi, const uint8_t*
   // per-wave points and digits, then the failing groups' vote list (count word, entries)
   const size_t list_off = align256((size_t)grid * nwc::MSM_WAVE_BYTES);
   const size_t need = list_off + 256 + 4 * nvotes;
-  if (need > d.msm_cap) {
-    HIP_TRY(hipStreamSynchronize(s));
-    if (d.msm_scratch) HIP_TRY(hipFree(d.msm_scratch));
-    d.msm_scratch = nullptr;
-    d.msm_cap = 0;
-    HIP_TRY(hipMalloc(&d.msm_scratch, need));
-    d.msm_cap = need;
-  }
+  if (int rc = release_idle_buffers(d, d.msm_scratch)) return rc;
+  if (int rc = ensure_buf(d, d.msm_scratch, d.msm_cap, need, s)) return rc;
   if (!d.msm_stats) {
     HIP_TRY(hipMalloc(&d.msm_stats, 4 * nwc::MSM_ST_WORDS));
     HIP_TRY(hipMemsetAsync(d.msm_stats, 0, 4 * nwc::MSM_ST_WORDS, s));
   }
   uint32_t* const mcount = reinterpret_cast<uint32_t*>(d.msm_scratch + list_off);
   uint32_t* const mlist = mcount + 64;
-  // the failing groups' votes: Straus sub-batches over the list (runs cut on the device), then the
-  // leaves for the sub-batches that fail -- a group with one bad vote costs ~12 leaf equations, not
-  // one per vote of the group
-  const uint32_t target = std::max<uint32_t>(1, std::min<uint32_t>(knobs().straus_nq.load(), nwc::STRAUS_MAX_PER_LANE));
-  const uint64_t sresident = (uint64_t)d.cus * nwc::STRAUS_WAVES_PER_SIMD * 256;
-  const uint64_t slanes = std::min<uint64_t>(((nvotes + target - 1) / target + 255) / 256 * 256, sresident);
-  const uint64_t sstride = (uint64_t)nwc::STRAUS_MAX_PER_LANE * nwc::STRAUS_VOTE_BYTES;   // runs cut on the device
-  if (int rc = ensure_straus_scratch(d, slanes * sstride, s)) return rc;
+  // the failing groups' votes go straight to the exact leaves (list mode): a vote meets at most one
+  // random equation, its group's
   const uint64_t lgrid = (uint64_t)d.cus * d.verify_blocks_per_cu;
   if (int rc = ensure_scratch(d, (size_t)lgrid * 256 * 2 * nwc::TAB_BYTES_PER_LANE, nvotes)) return rc;
   HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
   nwc::MsmArgs ma{};
   ma.digests = dig; ma.msg_index = mi; ma.pks = pks; ma.sigs = sigs; ma.nv = nvotes; ma.group = group;
-  {
-    // 32 bytes from the host's CSPRNG per launch (dalek: merlin transcript + thread_rng)
-    static thread_local std::random_device rd;
-    for (int i = 0; i < 8; ++i) ma.seed[i] = rd();
-  }
+  draw_seed(ma.seed);
   ma.comb16 = d.comb16; ma.scratch = d.msm_scratch;
   ma.leaf_words = leaf; ma.list = mlist; ma.count = mcount; ma.stats = d.msm_stats;
   HIP_TRY(hipMemsetAsync(leaf, 0, 8 * ((nvotes + 63) / 64), s));
   HIP_TRY(hipMemsetAsync(mcount, 0, sizeof(uint32_t), s));
-  HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
   hipLaunchKernelGGL(nwc::k_verify_msm, dim3((unsigned)grid), dim3(64), 0, s, ma);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(nwc::k_msm_policy, dim3(1), dim3(64), 0, s, d.msm_stats, (uint32_t)knobs().msm_adapt.load());
   HIP_TRY(hipGetLastError());
-  nwc::StrausArgs sa{};
-  sa.digests = dig; sa.msg_index = mi; sa.pks = pks; sa.sigs = sigs;
-  for (int i = 0; i < 8; ++i) sa.seed[i] = ma.seed[i] ^ 0x5a5a5a5au;   // fresh z for the second equation
-  sa.comb16 = d.comb16; sa.scratch = d.straus_scratch; sa.lane_stride = sstride;
-  sa.leaf_words = leaf; sa.list = d.uc_list; sa.count = d.uc_count;
-  sa.in_list = mlist; sa.in_count = mcount; sa.target = target;
-  hipLaunchKernelGGL(nwc::k_verify_straus<true>, dim3((unsigned)(slanes / 256)), dim3(256), 0, s, sa);
-  HIP_TRY(hipGetLastError());
   const nwc::VerifyArgs a{dig, mi, 0, pks, sigs, leaf, nvotes, 0, d.base_table, d.base24, d.scratch, d.fb_list,
                           d.fb_count, 0u, nwc::Committee{}};
-  const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16};
+  const nwc::CombArgs ca{mlist, mcount, d.comb_base, d.comb16};
   hipLaunchKernelGGL((nwc::k_verify<true, false, true>), dim3((unsigned)lgrid), dim3(256), 0, s, a, ca);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(16), dim3(256), 0, s, a);
   HIP_TRY(hipGetLastError());
-  if (int rc = launch_torsion(d, pks, leaf, nvotes, d.uc_list, d.uc_count, nwc::Committee{}, s)) return rc;
+  if (int rc = launch_torsion(d, pks, leaf, nvotes, mlist, mcount, nwc::Committee{}, s)) return rc;
   HIP_TRY(hipEventRecord(d.scratch_free, s));
   return 0;
+}
+
+// dalek's batch equation per certificate over the votes the leaves rejected (resolve.h), on s after
+// the leaves wrote `leaf` (bit per vote of m certificates): cm = the key set whose combs the leaves
+// used (nullptr combs: the ladder).  Sets the bits of the failing votes of certificates the equation
+// accepts.  Caller holds d.mu and has set the device.
+int launch_resolve(DevCtx& d, const uint8_t* dig, const uint32_t* mi, uint64_t m, const uint8_t* pks,
+                   const uint8_t* sigs, uint64_t nv, uint64_t* leaf, const nwc::Committee& cm, hipStream_t s) {
+  if (nv == 0) return 0;
+  if (nv > 0xFFFFFFFFull || m > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "more than 2^32 - 1 votes or certificates");
+  const size_t state_off = align256(256 + 4 * (size_t)nv);
+  if (int rc = release_idle_buffers(d, d.rs_buf)) return rc;
+  if (int rc = ensure_buf(d, d.rs_buf, d.rs_cap, state_off + align256(4 * (size_t)m), s)) return rc;
+  // one lane per failing vote; a lane slot's ladder table lives in the verification scratch
+  const uint64_t grid = (uint64_t)d.cus * d.verify_blocks_per_cu;
+  if (int rc = ensure_scratch(d, (size_t)grid * 256 * 2 * nwc::TAB_BYTES_PER_LANE, std::min(nv, verify_max_launch())))
+    return rc;
+  HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
+  uint32_t* const count = reinterpret_cast<uint32_t*>(d.rs_buf);
+  uint32_t* const list = count + 64;
+  uint32_t* const state = reinterpret_cast<uint32_t*>(d.rs_buf + state_off);
+  HIP_TRY(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(state, 0, 4 * (size_t)m, s));
+  const uint64_t words = (nv + 63) / 64;
+  hipLaunchKernelGGL(nwc::k_list_failing, dim3((unsigned)std::min<uint64_t>((words + 255) / 256, (uint64_t)d.cus * 8)),
+                     dim3(256), 0, s, leaf, nv, list, count);
+  HIP_TRY(hipGetLastError());
+  nwc::ResolveArgs ra{};
+  ra.digests = dig; ra.msg_index = mi; ra.pks = pks; ra.sigs = sigs; ra.list = list; ra.count = count;
+  draw_seed(ra.seed);
+  ra.cm = cm; ra.comb16 = d.comb16; ra.base_table = d.base_table; ra.scratch = d.scratch;
+  ra.cert_state = state; ra.leaf_words = leaf;
+  hipLaunchKernelGGL(nwc::k_vote_resolve, dim3((unsigned)grid), dim3(256), 0, s, ra);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(nwc::k_resolve_apply, dim3((unsigned)(d.cus * 2)), dim3(256), 0, s, ra);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(d.scratch_free, s));
+  return 0;
+}
+
+// Signature::verify_batch over m certificates with dalek's batch semantics (crypto/src/lib.rs:218).
+// Where key combs apply (a committee cache with combs, or a launch large enough for launch keys):
+// the exact per-vote leaves on the comb path, then dalek's equation once per certificate over the
+// votes they rejected (launch_resolve) -- every vote meets one random equation, its certificate's.
+// Otherwise the Pippenger groups first (launch_msm).  Caller holds d.mu and has set the device.
+int launch_batch_dalek(DevCtx& d, const uint8_t* dig, const uint32_t* mi, uint64_t m, const uint8_t* pks,
+                       const uint8_t* sigs, uint64_t nv, uint64_t* leaf, hipStream_t s) {
+  if (nv == 0) return 0;
+  if (int rc = ensure_verify_tables(d)) return rc;
+  const bool committee = d.cm_n && d.cm_comb;
+  const bool lkeys = !d.cm_n && nv >= nwc::LK_MIN_EQUATIONS && knobs().launch_keys.load();
+  if (verify_path() != VPath::Default || !d.comb16 || !(committee || lkeys))
+    return launch_msm(d, dig, mi, pks, sigs, nv, leaf, s);
+  if (int rc = launch_verify(d, dig, mi, 0, pks, sigs, nv, 0, leaf, s)) return rc;
+  const nwc::Committee cm = committee ? nwc::Committee{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots,
+                                                       d.cm_slot_mask, d.cm_n}
+                                      : nwc::Committee{d.lk.keys, d.lk.flags, nullptr, d.lk.comb, d.lk.slots,
+                                                       nwc::LK_SLOTS - 1, nwc::LK_MAX_KEYS};
+  return launch_resolve(d, dig, mi, m, pks, sigs, nv, leaf, cm, s);
 }
 
 // Per-vote leaf bits of every device's share (whole certificates) -> certificate verdicts and the
@@ -1524,7 +1662,9 @@ int straus_range(int di, const uint8_t* digests, size_t m, const uint32_t* offse
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(dp, pks + 32 * lo, 32 * n, hipMemcpyHostToDevice, d.stream));
   HIP_TRY(hipMemcpyAsync(ds, sigs + 64 * lo, 64 * n, hipMemcpyHostToDevice, d.stream));
-  if (int rc = (msm ? launch_msm : launch_straus)(d, dm, dmi, dp, ds, n, dout, d.stream)) return rc;
+  if (int rc = msm ? launch_batch_dalek(d, dm, dmi, m, dp, ds, n, dout, d.stream)
+                   : launch_straus(d, dm, dmi, dp, ds, n, dout, d.stream))
+    return rc;
   HIP_TRY(hipMemcpyAsync(out_words.data(), dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
   HIP_TRY(hipStreamSynchronize(d.stream));
   return 0;
@@ -1579,6 +1719,8 @@ int nwc_diag_set(const char* name, int64_t value) {
   } else if (std::strcmp(name, "msm_adapt") == 0) {
     if (value > 1) return set_err(NWC_ERR_ARG, "msm_adapt must be 0 or 1");
     knobs().msm_adapt = (uint32_t)value;
+  } else if (std::strcmp(name, "dalek_seed") == 0) {
+    knobs().dalek_seed = (uint64_t)value;
   } else if (std::strcmp(name, "launch_keys") == 0) {
     if (value > 1) return set_err(NWC_ERR_ARG, "launch_keys must be 0 or 1");
     knobs().launch_keys = (uint32_t)value;
@@ -1654,12 +1796,19 @@ void nwc_shutdown(void) {
     if (d->ak_comb) (void)hipFree(d->ak_comb);
     if (d->ak_slots) (void)hipFree(d->ak_slots);
     if (d->comb_base) (void)hipFree(d->comb_base);
+    if (d->base_table) (void)hipFree(d->base_table);
+    if (d->base24) (void)hipFree(d->base24);
+    if (d->base24_points) (void)hipFree(d->base24_points);
+    if (d->km_keys) (void)hipFree(d->km_keys);
+    if (d->km_flag) (void)hipFree(d->km_flag);
     if (d->comb16) (void)hipFree(d->comb16);
     if (d->comb16_bases) (void)hipFree(d->comb16_bases);
     if (d->kb_bases) (void)hipFree(d->kb_bases);
     if (d->straus_scratch) (void)hipFree(d->straus_scratch);
     if (d->msm_scratch) (void)hipFree(d->msm_scratch);
+    if (d->rs_buf) (void)hipFree(d->rs_buf);
     if (d->msm_stats) (void)hipFree(d->msm_stats);
+    if (d->lk_demand) (void)hipHostFree(d->lk_demand);
     if (d->lk_alloc) {
       (void)hipFree(d->lk.keys);
       (void)hipFree(d->lk.flags);
@@ -2071,9 +2220,9 @@ int nwc_dev_verify_batch_msm(const void* d_digests, const void* d_offsets, const
   if (m == 0 || nvotes == 0) return 0;
   if (!d_digests || !d_offsets || !d_msg_index || !d_pks || !d_sigs || !d_leaf_words)
     return set_err(NWC_ERR_ARG, "null buffer");
-  return launch_msm(d, static_cast<const uint8_t*>(d_digests), static_cast<const uint32_t*>(d_msg_index),
-                    static_cast<const uint8_t*>(d_pks), static_cast<const uint8_t*>(d_sigs), nvotes,
-                    static_cast<uint64_t*>(d_leaf_words), s);
+  return launch_batch_dalek(d, static_cast<const uint8_t*>(d_digests), static_cast<const uint32_t*>(d_msg_index), m,
+                            static_cast<const uint8_t*>(d_pks), static_cast<const uint8_t*>(d_sigs), nvotes,
+                            static_cast<uint64_t*>(d_leaf_words), s);
 }
 
 int nwc_msm_stats(uint64_t* groups_passed, uint64_t* groups_failed, uint64_t* key_overflows, uint64_t* groups_skipped) {
@@ -2126,6 +2275,7 @@ int nwc_dev_keygen_sign(const void* d_seeds, const void* d_msgs, uint64_t n, voi
                         void* stream) {
   DEV_PROLOGUE
   if (n == 0) return 0;
+  if (int rc = ensure_verify_tables(d)) return rc;
   hipLaunchKernelGGL(nwc::k_keygen_sign, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const uint8_t*)d_seeds,
                      (const uint8_t*)d_msgs, n, (uint8_t*)d_pks, (uint8_t*)d_sigs, d.base_table);
   HIP_TRY(hipGetLastError());
@@ -2215,6 +2365,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
                         uint8_t* ddigests, uint32_t* drec, hipStream_t s,
                         const std::function<int(size_t)>& chunk_ready = nullptr,
                         const std::function<bool(size_t)>& chunk_queued = nullptr) {
+  if (int rc = ensure_verify_tables(d)) return rc;
   const size_t nch = cuts.size() - 1;
   // a vote list is allocated only when wholly inside its message (>= 72 B per vote)
   const uint64_t vt = total / 72 + 1 + (nch > 1 ? 64 * nch : 0);   // + the 64-slot alignment of each chunk
@@ -2460,6 +2611,7 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
   DevCtx& d = *ctx(di);
   std::lock_guard<std::mutex> lk(d.mu);
   HIP_TRY(hipSetDevice(d.hip_id));
+  if (int rc = ensure_verify_tables(d)) return rc;
   if (!d.cc_stakes) return set_err(NWC_ERR_NOT_INIT, "nwc_set_committee_config has not been called");
   // staging area (the arena): message bytes, offsets, codes, records, digests
   const size_t need = align256(total + 16) + align256(8 * (m + 1)) + align256(4 * m) + align256(16 * m) +
@@ -2636,18 +2788,20 @@ int nwc_memory_info(nwc_memory* out) {
   *out = nwc_memory{};
   {
     std::lock_guard<std::mutex> lk(d.mu);
-    out->tables = 2 * 129 * sizeof(nwc::ge_niels) + 2 * (size_t)nwc::B24_ENTRIES * sizeof(nwc::ge_niels_pad) +
+    // built by the first call that verifies or signs (ensure_verify_tables); 0 before
+    out->tables = !d.tables_ready ? 0 :
+                  2 * 129 * sizeof(nwc::ge_niels) + 2 * (size_t)nwc::B24_ENTRIES * sizeof(nwc::ge_niels_pad) +
                   2 * sizeof(nwc::ge_p3) + nwc::BaseComb::per * sizeof(nwc::ge_niels_pad) +
                   (d.comb16 ? nwc::COMB16_TOTAL * sizeof(nwc::ge_niels_pad) + nwc::COMB16_WINDOWS * sizeof(nwc::ge_p3) : 0) +
                   36 * (size_t)NWC_MEMO_SLOTS;
     out->committee = d.cm_bytes;
     out->auto_cache = (size_t)d.ak_cap * (36 + 129 * sizeof(nwc::ge_niels) + nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad)) +
                       4 * (size_t)d.ak_slot_cap + d.kb_cap * sizeof(nwc::ge_p3) +
-                      (d.lk_alloc ? (size_t)nwc::LK_MAX_KEYS * (36 + nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad) +
-                                                               nwc::KeyComb::windows * sizeof(nwc::ge_p3)) +
+                      (d.lk_alloc ? (size_t)nwc::LK_MAX_KEYS * (36 + nwc::KeyComb::windows * sizeof(nwc::ge_p3)) +
+                                        (size_t)d.lk.cap * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad) +
                                         4 * (size_t)nwc::LK_SLOTS + 16
                                   : 0);
-    out->scratch = d.scratch_cap + d.straus_cap + d.msm_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap +
+    out->scratch = d.scratch_cap + d.straus_cap + d.msm_cap + d.rs_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap +
                    8 * (size_t)d.ts_slot_count;
   }
   out->digesters = digester_device_bytes(d.hip_id);
@@ -2672,6 +2826,8 @@ int nwc_trim(void) {
   if (d.straus_scratch) HIP_TRY(hipFree(d.straus_scratch));
   if (d.msm_scratch) HIP_TRY(hipFree(d.msm_scratch));
   d.msm_scratch = nullptr; d.msm_cap = 0;
+  if (d.rs_buf) HIP_TRY(hipFree(d.rs_buf));
+  d.rs_buf = nullptr; d.rs_cap = 0;
   if (d.arena) HIP_TRY(hipFree(d.arena));
   if (d.msg_arena) HIP_TRY(hipFree(d.msg_arena));
   d.scratch = nullptr; d.scratch_cap = 0;

@@ -271,6 +271,63 @@ def verify_batch_dalek_sampled(msg: bytes, votes: Sequence[Tuple[bytes, bytes]],
     return acc == IDENTITY
 
 
+def verify_batch_dalek_z(msg: bytes, votes: Sequence[Tuple[bytes, bytes]], zs: Sequence[int]) -> bool:
+    """dalek 1.0.1 `verify_batch`'s equation (crypto/src/lib.rs:218) for GIVEN 128-bit z_i, as the
+    crate computes it: -(sum z_i s_i mod l) B + sum z_i R_i + sum (z_i k_i mod l) A_i == O."""
+    bcoef, acc = 0, IDENTITY
+    for (pk, sig), z in zip(votes, zs):
+        if not sig_scalar_ok(sig):
+            return False
+        A = decompress(pk)
+        R = decompress(sig[:32])
+        if A is None or R is None:
+            return False
+        k = scalar_from_hash(sha512(sig[:32] + pk + msg))
+        s = int.from_bytes(sig[32:], "little")
+        bcoef = (bcoef + z * s) % L
+        acc = pt_add(acc, pt_add(pt_mul(z, R), pt_mul(z * k % L, A)))
+    acc = pt_add(acc, pt_mul((-bcoef) % L, BASEPOINT))
+    return acc == IDENTITY
+
+
+# The order-8 point G8 that generates E[8] (y = the fourth small-order y of SURVEY.md A.3, x even).
+G8_HEX = "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05"
+
+
+def torsion_dlog(p: Point) -> Optional[int]:
+    """j in 0..7 with p == [j] G8, or None when p is not in E[8] (E[8] is cyclic of order 8)."""
+    g = decompress(bytes.fromhex(G8_HEX))
+    acc = IDENTITY
+    for j in range(8):
+        if acc == p:
+            return j
+        acc = pt_add(acc, g)
+    return None
+
+
+def verify_batch_z8(msg: bytes, votes: Sequence[Tuple[bytes, bytes]], zs: Sequence[int]) -> bool:
+    """The same equation for the same z_i, evaluated the way the GPU resolves it
+    (narwhal_amd/csrc/resolve.h): with z_i k_i = (z_i k_i mod l) + q_i l and e_i = s_i B - R_i - k_i A_i
+    the left side is -sum (z_i e_i + q_i (l A_i)).  A vote that does not parse or decode, or whose
+    e_i has a prime-order component, fails the equation (w.p. 1 - 2^-125; decided as Err); the
+    others have e_i = [a_i] G8 and l A_i = [b_i] G8, and the equation holds iff
+    sum (z_i a_i + q_i b_i) = 0 mod 8."""
+    total = 0
+    for (pk, sig), z in zip(votes, zs):
+        e = residual(msg, pk, sig)
+        if e is None or pt_mul(8, e) != IDENTITY:
+            return False
+        k = scalar_from_hash(sha512(sig[:32] + pk + msg))
+        q = (z * k) // L
+        total += z * torsion_dlog(e) + q * torsion_dlog(pt_mul(L, decompress(pk)))
+    return total % 8 == 0
+
+
+def batch_z(seed32: bytes, v: int) -> int:
+    """The GPU's z_i (narwhal_amd/csrc/straus.h straus_z): SHA-512(seed || u64le(v))[..16], little-endian."""
+    return int.from_bytes(sha512(seed32 + v.to_bytes(8, "little"))[:16], "little")
+
+
 # ----------------------------------------------------------------------------- signing
 def secret_expand(seed: bytes) -> Tuple[int, bytes]:
     h = sha512(seed)

@@ -560,6 +560,91 @@ int orc_verify_batch_straus(const u8 msg32[32], const u8 *pks, const u8 *sigs, s
   return ok;
 }
 
+/* dalek 1.0.1 verify_batch's equation for GIVEN 128-bit z_i (16 little-endian bytes each), term
+   by term as the crate states it:  -(sum z_i s_i mod l) B + sum z_i R_i + sum (z_i k_i mod l) A_i
+   == O (plain double-and-add per term; the test reference for orc_batch_z8).  1 = holds. */
+int orc_batch_eq_z(const u8 msg32[32], const u8 *pks, const u8 *sigs, size_t n, const u8 *zs) {
+  ensure_init();
+  static const u8 Z[32] = {0};
+  u8 bsc[32] = {0};
+  ge acc = ge_identity();
+  for (size_t i = 0; i < n; ++i) {
+    const u8 *pk = pks + 32 * i, *sig = sigs + 64 * i;
+    ge A, R;
+    if (!sig_scalar_ok(sig) || !ge_decompress(&A, pk) || !ge_decompress(&R, sig)) return 0;
+    u8 hh[64], k[32], z[32] = {0}, zk[32], t[32];
+    sha512_ctx c; sha512_init(&c);
+    sha512_update(&c, sig, 32); sha512_update(&c, pk, 32); sha512_update(&c, msg32, 32);
+    sha512_final(&c, hh);
+    sc_reduce512(k, hh);
+    memcpy(z, zs + 16 * i, 16);
+    sc_muladd(zk, z, k, Z);
+    sc_muladd(t, z, sig + 32, bsc);
+    memcpy(bsc, t, 32);
+    acc = ge_add(acc, ge_add(ge_scalarmult(z, R), ge_scalarmult(zk, A)));
+  }
+  u8 nb[32];
+  sc_neg(nb, bsc);
+  acc = ge_add(acc, ge_scalarmult(nb, BASE));
+  return ge_is_identity(acc);
+}
+
+/* j in 0..7 with p == [j] G8 (G8: the order-8 point with y = 26e8958f..6d53fc05, x even), -1 if
+   p is not in E[8] */
+static int torsion_dlog(ge p) {
+  static const u8 G8[32] = {0x26, 0xe8, 0x95, 0x8f, 0xc2, 0xb2, 0x27, 0xb0, 0x45, 0xc3, 0xf4, 0x89, 0xf2, 0xef, 0x98, 0xf0,
+                            0xd5, 0xdf, 0xac, 0x05, 0xd3, 0xc6, 0x33, 0x39, 0xb1, 0x38, 0x02, 0x88, 0x6d, 0x53, 0xfc, 0x05};
+  ge g, acc = ge_identity();
+  if (!ge_decompress(&g, G8)) return -1;
+  for (int j = 0; j < 8; ++j) {
+    if (ge_eq(acc, p)) return j;
+    acc = ge_add(acc, g);
+  }
+  return -1;
+}
+
+/* The same equation for the same z_i, evaluated in E[8] = Z/8 as the GPU resolves it
+   (narwhal_amd/csrc/resolve.h): -sum (z_i e_i + q_i (l A_i)) with e_i = s_i B - R_i - k_i A_i and
+   z_i k_i = (z_i k_i mod l) + q_i l.  A vote that does not parse or decode, or whose e_i is not
+   pure torsion, fails it (decided: Err w.p. 1 - 2^-125); otherwise e_i = [a_i] G8, l A_i = [b_i] G8
+   and the equation holds iff sum (z_i a_i + q_i b_i) = 0 mod 8 (q_i mod 8 = (z_i k_i - (z_i k_i
+   mod l)) / l mod 8 = 5 ((z_i k_i mod 8) - (z_i k_i mod l mod 8)) mod 8, since 1/l = 5 mod 8). */
+int orc_batch_z8(const u8 msg32[32], const u8 *pks, const u8 *sigs, size_t n, const u8 *zs) {
+  ensure_init();
+  static const u8 Z[32] = {0};
+  unsigned total = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const u8 *pk = pks + 32 * i, *sig = sigs + 64 * i;
+    ge A, R;
+    if (!sig_scalar_ok(sig) || !ge_decompress(&A, pk) || !ge_decompress(&R, sig)) return 0;
+    u8 hh[64], k[32], z[32] = {0}, zk[32];
+    sha512_ctx c; sha512_init(&c);
+    sha512_update(&c, sig, 32); sha512_update(&c, pk, 32); sha512_update(&c, msg32, 32);
+    sha512_final(&c, hh);
+    sc_reduce512(k, hh);
+    ge e = ge_add(ge_double_scalarmult_vartime(k, ge_neg(A), sig + 32), ge_neg(R));
+    if (!ge_is_small_order(e)) return 0;
+    memcpy(z, zs + 16 * i, 16);
+    sc_muladd(zk, z, k, Z);
+    const unsigned z8 = z[0] & 7u, q8 = (5u * ((z8 * (k[0] & 7u) + 8u - (zk[0] & 7u)) & 7u)) & 7u;
+    const int de = torsion_dlog(e), dl = torsion_dlog(ge_scalarmult(L_BYTES, A));
+    if (de < 0 || dl < 0) return 0;
+    total += z8 * (unsigned)de + q8 * (unsigned)dl;
+  }
+  return (total & 7u) == 0;
+}
+
+/* orc_batch_eq_z (which = 0) or orc_batch_z8 (which = 1) over m certificates (voffs, m + 1
+   offsets; zs: 16 bytes per vote), out[c] = 1 if the equation holds */
+void orc_batch_z_many(const u8 *digests, const u32 *voffs, const u8 *pks, const u8 *sigs, const u8 *zs, size_t m,
+                      u8 *out, int which) {
+  for (size_t c = 0; c < m; ++c) {
+    const u32 a = voffs[c], n = voffs[c + 1] - a;
+    out[c] = (u8)(which ? orc_batch_z8(digests + 32 * c, pks + 32 * (size_t)a, sigs + 64 * (size_t)a, n, zs + 16 * (size_t)a)
+                        : orc_batch_eq_z(digests + 32 * c, pks + 32 * (size_t)a, sigs + 64 * (size_t)a, n, zs + 16 * (size_t)a));
+  }
+}
+
 /* ================================================================ signing (fixtures, data) */
 void orc_public_key(const u8 seed[32], u8 pk[32]) {
   ensure_init();

@@ -32,6 +32,7 @@ class Oracle:
         lib.orc_verify_batch_straus_many.argtypes = [vp, vp, vp, vp, sz, vp, ctypes.c_int]
         lib.orc_digest32_many_mt.argtypes = [vp, vp, sz, vp, ctypes.c_int]
         lib.orc_keygen_sign_many.argtypes = [vp, vp, sz, sz, vp, vp, ctypes.c_int]
+        lib.orc_batch_z_many.argtypes = [vp, vp, vp, vp, vp, sz, vp, ctypes.c_int]
 
     @staticmethod
     def _p(a):
@@ -98,6 +99,16 @@ class Oracle:
         offs = np.ascontiguousarray(offsets, dtype=np.uint32)
         self.lib.orc_verify_batch_straus_many(self._p(digests), self._p(offs), self._p(pks), self._p(sigs), m,
                                               self._p(out), threads)
+        return out.astype(bool)
+
+    def batch_z_many(self, digests: np.ndarray, offsets: np.ndarray, pks: np.ndarray, sigs: np.ndarray,
+                     zs: np.ndarray, z8: bool) -> np.ndarray:
+        """dalek's batch equation per certificate for given z_i (zs: 16 bytes per vote), term by term
+        (orc_batch_eq_z) or in E[8] = Z/8 as the GPU resolves it (orc_batch_z8)."""
+        m = offsets.shape[0] - 1
+        out = np.zeros(m, dtype=np.uint8)
+        self.lib.orc_batch_z_many(self._p(digests), self._p(offsets.astype(np.uint32)), self._p(pks), self._p(sigs),
+                                  self._p(zs), m, self._p(out), 1 if z8 else 0)
         return out.astype(bool)
 
     def keygen_sign_many(self, seeds: np.ndarray, msgs: np.ndarray, threads: int = 8):

@@ -219,3 +219,135 @@ def test_stamped_clock_launch():
     exp = (np.arange(n) % (1 << 12)) % 7 != 0
     assert (device.unpack_bits(words, n) == exp).all()
     print("in-kernel clock %.3f GHz over %d waves" % (ghz, waves))
+
+
+def test_digest_only_process_holds_no_tables():
+    """A worker process that only digests (worker/src/worker.rs:182-188: workers and a primary share
+    the GPU) holds no verification tables: they are built by the first call that verifies.  A fresh
+    process (the tables are per process): digests through the digester and the many-entry, then
+    nwc_memory_info shows tables == 0 and no key caches; one verification builds them."""
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    code = r'''
+import sys, hashlib; sys.path.insert(0, %r)
+import numpy as np, torch
+from narwhal_amd import _lib, crypto
+from narwhal_amd.processor import Digester
+lib = _lib.load()
+assert _lib.memory_info()["tables"] == 0, _lib.memory_info()
+rng = np.random.default_rng(5)
+msgs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in rng.integers(0, 600000, 40)]
+got = crypto.digest_many(msgs)
+assert [g.to_vec() for g in got] == [hashlib.sha512(m).digest()[:32] for m in msgs]
+dg = Digester(64, 1000)
+for i, m in enumerate(msgs):
+    dg.submit(m, i)
+out = []
+while len(out) < len(msgs):
+    out += dg.poll(64, 100000)
+assert [d for _, d in sorted(out)] == [hashlib.sha512(m).digest()[:32] for m in msgs]
+mem = _lib.memory_info()
+dg.close()
+assert mem["tables"] == 0 and mem["auto_cache"] == 0 and mem["committee"] == 0, mem
+print("digest-only", mem, flush=True)
+import json
+gold = json.load(open(%r))
+c = [c for c in gold["cases"] if c["name"] == "ref-verify_valid_signature"][0]
+assert lib.nwc_verify_strict(bytes.fromhex(c["msg"]), bytes.fromhex(c["pk"]), bytes.fromhex(c["sig"])) == 0
+mem2 = _lib.memory_info()
+assert mem2["tables"] > (2 << 30), mem2
+print("after one verify", mem2, flush=True)
+''' % (ROOT, os.path.join(ROOT, "tests", "golden", "ed25519_verify.json"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    print(r.stdout)
+
+
+def test_batch_entry_buffers_above_keep_are_released():
+    """The Straus tables (~3.8 GB at config-3 size) and the MSM groups' scratch (~1.3 GB) stay only
+    while their entry runs: the next launch of another path frees them (NWC_VERIFY_KEEP_BYTES), so
+    scratch returns to the leaf path's own; verdicts equal the construction throughout."""
+    import torch
+    from narwhal_amd import _lib, device
+    lib = _lib.load()
+    _lib.check(lib.nwc_set_committee(None, 0))
+    _lib.check(lib.nwc_trim())
+    M, Q = 6000, 67
+    nv = M * Q
+    cdig = device.derive32(b"keep-cert", 0, M)
+    seeds = device.derive32(b"keep-seed", 0, 100)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    who = torch.randint(0, 100, (nv,), device="cuda", generator=g)
+    bad = torch.rand(nv, device="cuda", generator=g) < 0.01
+    mi = torch.arange(M, device="cuda", dtype=torch.int32).repeat_interleave(Q)
+    signed = cdig[mi.long()].clone()
+    signed[bad, 3] ^= 1
+    pks, sigs = device.keygen_sign(seeds[who], signed)
+    offs = torch.arange(M + 1, device="cuda", dtype=torch.int32) * Q
+    want = bad.cpu().numpy()
+
+    def leaves():
+        return device.verify(cdig, pks, sigs, strict=False, msg_index=mi)
+
+    _lib.diag_set("launch_keys", 0)
+    _lib.diag_set("msm_adapt", 0)
+    try:
+        assert (~device.unpack_bits(leaves(), nv) == want).all()
+        torch.cuda.synchronize()
+        base = _lib.memory_info()["scratch"]
+        for f in (device.verify_batch_straus, device.verify_batch_msm):
+            w = f(cdig, offs, mi, pks, sigs)
+            torch.cuda.synchronize()
+            _, bw = device.cert_reduce(w, offs, nv)
+            assert (device.unpack_bits(bw, nv) == want).all(), f.__name__
+            held = _lib.memory_info()["scratch"]
+            assert held - base > (256 << 20), (f.__name__, base, held)
+            assert (~device.unpack_bits(leaves(), nv) == want).all()
+            torch.cuda.synchronize()
+            after = _lib.memory_info()["scratch"]
+            assert after - base < (256 << 20), (f.__name__, base, held, after)
+            print("%s: scratch base %.0f MB, with the entry's buffers %.0f MB, after a leaf launch %.0f MB"
+                  % (f.__name__, base / 2**20, held / 2**20, after / 2**20))
+    finally:
+        _lib.diag_set("launch_keys", 1)
+        _lib.diag_set("msm_adapt", 1)
+
+
+def test_launch_key_combs_grow_as_keys_join():
+    """Launch-key combs are allocated for the keys that join (20 MB each), not for 128 up front: a
+    launch over 40 repeated keys reserves room for 40; a launch that brings 60 more runs them on the
+    ladder (room for 40) and records the demand; the next grows the combs and they join.  Verdicts
+    equal the construction at every step (launch_keys.h)."""
+    import ctypes
+    import torch
+    from narwhal_amd import _lib, device
+    lib = _lib.load()
+    _lib.check(lib.nwc_set_committee(None, 0))
+    _lib.check(lib.nwc_trim())
+    seeds = device.derive32(b"grow-seed", 0, 100)
+
+    def launch(nkeys, n=1 << 17, tag=0):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(100 + tag)
+        who = torch.randint(0, nkeys, (n,), device="cuda", generator=g)
+        msgs = device.derive32(b"grow-msg%d" % tag, 0, n)
+        pks, sigs = device.keygen_sign(seeds[who], msgs)
+        sigs[::97, 5] ^= 1
+        got = device.unpack_bits(device.verify(msgs, pks, sigs, strict=False), n)
+        torch.cuda.synchronize()
+        exp = np.ones(n, bool)
+        exp[::97] = False
+        assert (got == exp).all()
+        h = ctypes.c_uint32()
+        _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
+        return h.value, _lib.memory_info()["auto_cache"]
+
+    comb = 155648 * 128   # KeyComb: 19 windows x 8,192 entries of 128 B
+    h1, m1 = launch(40, tag=1)
+    h2, m2 = launch(100, tag=2)
+    h3, m3 = launch(100, tag=3)
+    assert (h1, h2, h3) == (40, 40, 100), (h1, h2, h3)
+    assert m2 == m1 and m3 - m1 >= 60 * comb and m3 < m1 + 70 * comb, (m1, m2, m3)
+    assert m1 < 48 * comb + (400 << 20), m1

@@ -226,3 +226,55 @@ def test_c_oracle_naf_regression():
     import numpy as np
     assert o.batch_straus_many(np.frombuffer(m, np.uint8).reshape(1, 32), np.array([0, 1], np.uint32),
                                np.frombuffer(p, np.uint8).reshape(1, 32), np.frombuffer(s, np.uint8).reshape(1, 64)).all()
+
+
+def _z_draws(rng, n):
+    return rng.integers(0, 256, (n, 16), dtype=np.uint8)
+
+
+def test_batch_z8_equals_dalek_equation(oracle, golden_verify, golden_batch):
+    """The per-certificate resolution of dalek's batch equation in E[8] = Z/8 (orc_batch_z8, what
+    narwhal_amd/csrc/resolve.h computes on the GPU) equals the equation evaluated term by term as
+    the crate states it (orc_batch_eq_z) for the same z_i -- 60 draws of z over every golden batch
+    and every strict case as a one-vote batch (crypto/src/lib.rs:206-219).  Both outcomes occur on
+    the randomized class."""
+    rng = np.random.default_rng(77)
+    D = 60
+    seen = {}
+    for name, m, votes, cls in _golden_batches(golden_verify, golden_batch):
+        n = len(votes)
+        if n == 0:
+            continue
+        digests = np.tile(np.frombuffer(m, dtype=np.uint8), (D, 1))
+        offs = (np.arange(D + 1) * n).astype(np.uint32)
+        pks = np.tile(np.frombuffer(b"".join(p for p, _ in votes), dtype=np.uint8).reshape(-1, 32), (D, 1))
+        sigs = np.tile(np.frombuffer(b"".join(s for _, s in votes), dtype=np.uint8).reshape(-1, 64), (D, 1))
+        zs = _z_draws(rng, D * n)
+        full = oracle.batch_z_many(digests, offs, pks, sigs, zs, z8=False)
+        z8 = oracle.batch_z_many(digests, offs, pks, sigs, zs, z8=True)
+        assert (full == z8).all(), (name, full.sum(), z8.sum())
+        seen.setdefault(cls, []).append(int(z8.sum()))
+        if cls == "ok":
+            assert z8.all(), name
+        elif cls == "err":
+            assert not z8.any(), name
+    assert any(0 < a < D for a in seen["randomized"]), seen["randomized"]
+
+
+def test_batch_z8_python_restatement(oracle, golden_batch):
+    """The C resolution against the Python restatement's (which takes q_i = floor(z_i k_i / l) as a
+    big integer rather than mod 8) on the randomized golden batches, one draw each."""
+    import random
+    rng = random.Random(78)
+    for b in golden_batch:
+        if b["class"] != "randomized":
+            continue
+        votes = [(bytes.fromhex(p), bytes.fromhex(s)) for p, s in b["votes"]]
+        m = bytes.fromhex(b["msg"])
+        for _ in range(1):
+            zs = [rng.getrandbits(128) for _ in votes]
+            zb = np.frombuffer(b"".join(z.to_bytes(16, "little") for z in zs), np.uint8).reshape(-1, 16)
+            got = oracle.batch_z_many(np.frombuffer(m, np.uint8)[None, :], np.array([0, len(votes)], np.uint32),
+                                      np.frombuffer(b"".join(p for p, _ in votes), np.uint8).reshape(-1, 32),
+                                      np.frombuffer(b"".join(s for _, s in votes), np.uint8).reshape(-1, 64), zb, z8=True)
+            assert bool(got[0]) == pyref.verify_batch_z8(m, votes, zs), b["name"]
