@@ -61,14 +61,15 @@ CFG4_BATCH_BYTES = 12 + CFG4_TXS * (8 + CFG4_TX_BYTES)   # 508,052
 CFG4_STRIDE = (CFG4_BATCH_BYTES + 255) & ~255
 
 
-PROFILE_ROUND = "r05"   # profiles/<round>/summary.json: rocprofv3 PMC passes of this build
+PROFILE_ROUND = "r06"   # profiles/<round>/<workload>/summary.json: rocprofv3 passes of this build (tools/profile_r06.sh)
 
 
-def profile_counters(*kernel_names: str):
-    """Per-launch PMC figures of `kernel_prefix` from the committed rocprofv3 summary
-    (tools/profile_round.sh -> tools/summarize_profile.py): HBM traffic = FETCH_SIZE x2 (gfx950
-    wide-read correction) + WRITE_SIZE, and the hardware VALU issue fraction.  None if absent."""
-    path = os.path.join(ROOT, "profiles", PROFILE_ROUND, "summary.json")
+def profile_counters(*kernel_names: str, workload: str = "head"):
+    """Per-launch PMC figures of the first of `kernel_names` found in the committed rocprofv3 summary
+    of `workload` (tools/profile_r06.sh -> tools/summarize_profile.py): HBM traffic = FETCH_SIZE x2
+    (gfx950 wide-read correction) + WRITE_SIZE, VALU lane-ops per launch, the average duration and
+    the shader clock during the kernel (GRBM_GUI_ACTIVE per XCD / duration).  None if absent."""
+    path = os.path.join(ROOT, "profiles", PROFILE_ROUND, workload, "summary.json")
     try:
         summ = json.load(open(path))
     except (OSError, ValueError):
@@ -78,11 +79,21 @@ def profile_counters(*kernel_names: str):
         if "hbm_traffic_bytes_per_launch" in d:
             return {"traffic": d["hbm_traffic_bytes_per_launch"], "valu_insts_per_lane": d.get("valu_insts_per_lane"),
                     "lane_ops_per_launch": d.get("SQ_INSTS_VALU", 0) * 64, "avg_ns": d.get("avg_ns"),
-                    "source": "profiles/%s/summary.json (%s)" % (PROFILE_ROUND, k)}
+                    "calls": d.get("calls"), "clock_ghz": d.get("gui_active_clk_ghz_per_xcd"),
+                    "source": "profiles/%s/%s/summary.json (%s)" % (PROFILE_ROUND, workload, k)}
     return None
 
 
-CENSUS = os.path.join(ROOT, "profiles", "r05", "isa_census.json")   # tools/isa_census.py of this build
+def profile_kernel_ms(workload: str, kernel: str):
+    """Average duration (ms) of `kernel` in the committed kernel trace of `workload`, or None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", PROFILE_ROUND, workload, "summary.json"))).get(kernel, {})
+        return d["avg_ns"] * 1e-6
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+CENSUS = os.path.join(ROOT, "profiles", PROFILE_ROUND, "isa_census.json")   # tools/isa_census.py of this build
 
 
 def issue_cycles(kernel: str):
@@ -93,6 +104,48 @@ def issue_cycles(kernel: str):
         return k["avg_issue_cycles"], k["share_4cycle"]
     except (OSError, ValueError, KeyError):
         return None, None
+
+
+def roofline_extra(workload: str, kernel: str, census: str, units: int, unit: str, step_ms_live: float,
+                   units_per_step: int, algo_bytes_per_unit: float, extra_kernels=()):
+    """Roofline entry of a non-headline number (configs 3 and 5): the dominant kernel's VALU lane-ops
+    per launch (SQ_INSTS_VALU x 64) over its average duration, both from the committed rocprofv3
+    passes of this workload (`pmc_source`), against the guide's VALU issue peak (frac), priced per
+    instruction class by the ISA census (frac_issue), with the shader clock the kernel held
+    (GRBM_GUI_ACTIVE) and its HBM traffic per unit against the algorithmic input bytes.  Beside it,
+    the live step time of this run and the dalek work model per unit over it (effective_frac: W_strict
+    per unit / live step time; batch algorithms that do less work per vote exceed the hardware
+    fraction).  `units` = the units one launch of the kernel processes."""
+    out = {"bound": "valu", "unit": "T lane-ops/s", "peak": VALU_PEAK_TOPS, "kernel": kernel,
+           "units_per_launch": units, "unit_name": unit, "step_ms_live": step_ms_live,
+           "effective_frac": units_per_step / (step_ms_live * 1e-3) * ops_per_verify() / 1e12 / VALU_PEAK_TOPS,
+           "algorithmic_bytes_per_unit": algo_bytes_per_unit}
+    pc = profile_counters("nwc::" + kernel, workload=workload)
+    if not pc:
+        out.update({"frac": None, "pmc_source": "profiles/%s/%s/summary.json missing" % (PROFILE_ROUND, workload)})
+        return out
+    kms = pc["avg_ns"] * 1e-6
+    ach = pc["lane_ops_per_launch"] / (kms * 1e-3) / 1e12
+    out.update({"kernel_ms_rocprof": kms, "achieved": ach, "frac": ach / VALU_PEAK_TOPS,
+                "frac_vop3_rate": ach / VOP3_RATE_TOPS, "valu_insts_per_unit": pc["lane_ops_per_launch"] / units,
+                "traffic": pc["traffic"], "traffic_per_unit": pc["traffic"] / units,
+                "traffic_over_algorithmic": pc["traffic"] / (algo_bytes_per_unit * units),
+                "clock_ghz": pc["clock_ghz"], "pmc_source": pc["source"]})
+    cyc, share = issue_cycles(census) if census else (None, None)
+    if cyc:
+        out["frac_issue"] = out["frac"] * cyc / 2
+        out["issue_census"] = {"avg_issue_cycles": cyc, "share_4cycle": share,
+                               "source": os.path.relpath(CENSUS, ROOT) + " (tools/isa_census.py)"}
+        if pc["clock_ghz"]:
+            out["frac_issue_at_clock"] = out["frac_issue"] * 2.4 / pc["clock_ghz"]
+    others = {}
+    for k in extra_kernels:
+        ms = profile_kernel_ms(workload, "nwc::" + k)
+        if ms is not None:
+            others[k] = ms
+    if others:
+        out["other_kernels_ms_rocprof"] = others
+    return out
 
 
 def ops_per_verify() -> float:
@@ -483,7 +536,7 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
     sub-batches), with the launch keys the library detects itself (no nwc_set_committee: first
     launch incl. the census and the 100 keys' comb builds, then steady state), and with the
     committee key cache."""
-    from narwhal_amd import _lib
+    from narwhal_amd import _lib, device
     import torch
     inst = make_cfg3(m)
     N, Q, nv = inst["N"], inst["Q"], inst["nv"]
@@ -563,6 +616,14 @@ def bench_cfg3(lib, m: int, steps: int, cpu_budget: float = 0.0):
             h = ctypes.c_uint32()
             _lib.check(lib.nwc_launch_keys_info(ctypes.byref(h), None))
             out[tag]["launch_keys_held"] = h.value
+        # input bytes per vote: key 32 + signature 64 + its certificate index 4 + a 67th of a digest
+        prof = {"launch_keys": ("c3lk", "k_verify_comb", "k_verify_comb", ()),
+                "dalek_launch_keys": ("c3dk", "k_verify_comb", "k_verify_comb",
+                                      ("k_list_failing", "k_vote_resolve", "k_resolve_apply")),
+                "clean_no_cache_msm": ("c3msm", "k_verify_msm", None, ())}.get(tag)
+        if prof:
+            out[tag]["roofline"] = roofline_extra(prof[0], prof[1], prof[2], nv, "vote", dt * 1e3, nv,
+                                                  100 + 32.0 / Q, prof[3])
     _lib.check(lib.nwc_set_committee(None, 0))
     _lib.diag_set("launch_keys", 1)
     if not only or "host_abi_launch_keys" in only.split(","):
@@ -853,6 +914,9 @@ def bench_cfg5(lib, rank: int, world: int, total: int, steps: int, cpu_budget: f
            "verifies_per_s": total / dt, "ms_per_pass": dt * 1e3, "per_gpu": per, "scaling": "strong",
            "verdict_allgather_ms": gather_ms, "verdict_d2h_ms": d2h_ms, "allgather_needed": False,
            "edge_slots_per_gpu": int(slot.numel()), "parity_ok": bool(okt.item() == 1)}
+    # the strict kernel over launches of at most NWC_VERIFY_MAX_LAUNCH (16M) equations
+    out["roofline"] = roofline_extra("c5", "k_verify<true, false, false, false>", "k_verify", min(per, 16 << 20),
+                                     "verify", dt * 1e3, per, 128)
     if cpu_budget > 0 and rank == 0 and world == 1:
         # the restatement's verify_strict on every CPU the box grants, on a
         # prefix of the same mixed signatures (edge cases included), verdicts checked

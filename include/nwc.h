@@ -52,11 +52,14 @@ const char* nwc_build_id(void);
 
 /* ---- device memory (a primary and a worker may share one GPU) ------------------------ */
 /* Bytes held by this process on the calling thread's device (nwc_dev_set_device): tables =
- * basepoint tables built at nwc_init (radix-2^24 ladder tables 2.1 GB, radix-2^22 comb 3.2 GB
- * unless NWC_COMB16=0, small ones); committee = the nwc_set_committee cache (20 MB per key with
- * combs); auto_cache = the auto key cache (NWC_AUTO_KEYS); scratch = per-launch buffers grown on
- * demand (ladder tables, Straus tables, staging, message buffers); digesters = the device buffers
- * of live nwc_digesters on this device; device_free / device_total = hipMemGetInfo. */
+ * basepoint tables (radix-2^24 ladder tables 2.1 GB, radix-2^22 comb 3.2 GB unless NWC_COMB16=0,
+ * small ones), built by the first call that verifies or signs -- 0 in a process that only digests;
+ * committee = the nwc_set_committee cache (20 MB per key with combs); auto_cache = the auto key
+ * cache (NWC_AUTO_KEYS) and the launch keys (20 MB of comb per key that joined); scratch =
+ * per-launch buffers grown on demand (ladder tables, Straus tables, MSM groups, staging, message
+ * buffers; the batch entries' buffers above NWC_VERIFY_KEEP_BYTES are freed by the next launch of
+ * another path); digesters = the device buffers of live nwc_digesters on this device;
+ * device_free / device_total = hipMemGetInfo. */
 typedef struct nwc_memory {
   uint64_t tables, committee, auto_cache, scratch, digesters, device_free, device_total;
 } nwc_memory;
@@ -72,7 +75,10 @@ int nwc_trim(void);
  * NWC_LAUNCH_KEYS; nwc_launch_keys_info); "msm_group" = votes per Pippenger group of the MSM
  * entry (a multiple of 64 in 64..4096; 0, the default = sized per launch; env NWC_MSM_GROUP);
  * "msm_adapt" = 0 / 1 (default 1, env NWC_MSM_ADAPT): the MSM entry's skip policy (0 = the
- * equation on every group).  NWC_ERR_ARG for an unknown name or value.
+ * equation on every group); "dalek_seed" = a fixed 32-bit seed of the batch entries' random z_i
+ * (z_i = SHA-512(seed as 4 LE bytes || 28 zero bytes || u64le(i))[..16]; 0, the default = 32 bytes
+ * of the host CSPRNG per launch), so tests can compute dalek's equation for the same z_i.
+ * NWC_ERR_ARG for an unknown name or value.
  * Not part of the crate's API. */
 int nwc_diag_set(const char* name, int64_t value);
 
@@ -120,14 +126,17 @@ int nwc_verify_batch_straus_many(const uint8_t* digests, const uint32_t* offsets
                                  const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap,
                                  uint8_t* bad_vote_bitmap);
 
-/* The same m certificates through dalek's batch equation as a Pippenger multi-scalar
- * multiplication over groups of up to 4,096 consecutive votes, one GPU wave per group
- * (nwc_dev_verify_batch_msm): random 128-bit z_i, the group's distinct keys aggregated (one point
- * per key), the R points bucketed in LDS with a wavefront-level bucket reduction; the votes of
- * the groups it rejects are re-decided by the exact per-vote leaves.  Verdicts and bad sets as
- * nwc_verify_batch_straus_many (deterministic domain exact; dalek's probabilities on its randomized
- * domain).  A group fails as a whole when any of its votes is bad, so it pays on clean traffic only
- * (DESIGN.md §4.2e). */
+/* The same m certificates with dalek's batch semantics (crypto/src/lib.rs:218):
+ * each certificate passes iff dalek's equation holds for it with random 128-bit z_i.  Where key
+ * combs apply (a committee cache, or >= 65,536 votes whose keys repeat: launch keys) every vote is
+ * first decided by the exact leaf on the comb path; then dalek's equation is evaluated once per
+ * certificate over the votes the leaves rejected (the others contribute the identity whatever
+ * z_i is), exactly, in the 8-torsion group -- the deterministic domain is the leaves' verdict, and
+ * on the randomized one (pure-torsion residuals, torsion-bearing keys) a certificate passes with
+ * dalek's probability, its failing votes then cleared from the bad set.  Otherwise the Pippenger
+ * MSM per group of up to 4,096 consecutive votes (nwc_dev_verify_batch_msm) decides first and the
+ * votes of the groups it rejects go to the exact leaves.  Every vote meets at most one random
+ * equation: its certificate's, or (no combs) its group's. */
 int nwc_verify_batch_msm_many(const uint8_t* digests, const uint32_t* offsets, const uint8_t* pks,
                               const uint8_t* sigs, size_t m, uint8_t* cert_ok_bitmap,
                               uint8_t* bad_vote_bitmap);
@@ -151,9 +160,11 @@ int nwc_auto_cache_info(uint32_t* capacity, uint64_t* builds, uint64_t* hits);
 
 /* Launch keys of the calling thread's device: a batch-leaf launch of >= 65,536 equations without a
  * committee cache samples its keys, and keys it repeats (>= ~1/4096 of the sample) join a
- * device-resident set with their flags and radix-2^14 combs (built once), so that votes of a
- * committee the caller never registered take the comb kernel -- cross-certificate key
- * aggregation, no nwc_set_committee needed.  Up to `capacity` keys; emptied by nwc_set_committee
+ * device-resident set with their flags and radix-2^14 combs (built once; room for 20 MB of comb
+ * per key is reserved as keys ask to join: the first launch measures its demand, later ones grow
+ * it from the demand the previous launch recorded, so a key that did not fit joins at the next
+ * launch), so that votes of a committee the caller never registered take the comb kernel --
+ * cross-certificate key aggregation, no nwc_set_committee needed.  Up to `capacity` keys; emptied by nwc_set_committee
  * and nwc_trim, and replaced by a launch whose repeated keys do not fit while the held ones cover
  * less than a quarter of its sample (a new committee); NWC_LAUNCH_KEYS=0 (or
  * nwc_diag_set("launch_keys", 0)) turns it off.
@@ -278,25 +289,26 @@ int nwc_dev_cert_reduce(const void* d_leaf_words, const void* d_offsets, uint64_
 int nwc_dev_verify_batch_straus(const void* d_digests, const void* d_offsets, const void* d_msg_index, uint64_t m,
                                 uint64_t nvotes, const void* d_pks, const void* d_sigs, void* d_leaf_words,
                                 void* stream);
-/* Signature::verify_batch over m certificates as dalek's batch equation evaluated by a Pippenger
- * MSM per group of consecutive votes (up to 4,096, sized so the groups fill whole rounds of the
- * resident waves; NWC_MSM_GROUP / nwc_diag_set("msm_group") fixes it): one wave per group sorts its
- * points into 512 buckets per 10-bit
- * window in LDS and reduces the buckets across its 64 lanes.  The votes of groups that fail go
- * through Straus sub-batches of ~12 (as nwc_dev_verify_batch_straus, fresh z_i), and those of
- * sub-batches that fail to the exact leaves.  Skip policy (device-side, no host synchronisation):
- * when more than half of a launch's groups fail (a bad-vote rate of about one per group or more),
- * the next 7 launches skip the equation and hand every vote straight to the sub-batches; the one
- * after them runs it on every group again and decides anew.  Same
- * arguments, leaf-word output and semantics as nwc_dev_verify_batch_straus (on dalek's randomized
- * domain a vote passes if its group or its sub-batch does: at most ~2/ord). */
+/* Signature::verify_batch over m certificates with dalek's batch semantics, device-resident (as
+ * nwc_verify_batch_msm_many).  With key combs (committee cache, or launch keys at >= 65,536 votes):
+ * the comb-path leaves, then dalek's equation per certificate over the leaves' failing votes, in
+ * E[8].  Without: dalek's batch equation as a Pippenger MSM per group of
+ * consecutive votes (up to 4,096, sized so the groups fill whole rounds of the resident waves;
+ * NWC_MSM_GROUP / nwc_diag_set("msm_group") fixes it): one wave per group sorts its points into 512
+ * buckets per 10-bit window in LDS and reduces the buckets across its 64 lanes; the votes of groups
+ * that fail go to the exact per-vote leaves (no second random equation: on dalek's randomized
+ * domain a vote passes iff its group's equation holds).  Skip policy (device-side, no host
+ * synchronisation; its state is per device, shared by every caller and stream of the device): when
+ * more than half of a launch's groups fail (a bad-vote rate of about one per group or more), the next
+ * 7 launches skip the equation and hand every vote straight to the leaves; the one after them runs
+ * it on every group again and decides anew.  d_leaf_words as nwc_dev_verify_batch_straus's. */
 int nwc_dev_verify_batch_msm(const void* d_digests, const void* d_offsets, const void* d_msg_index, uint64_t m,
                              uint64_t nvotes, const void* d_pks, const void* d_sigs, void* d_leaf_words,
                              void* stream);
 /* Groups of the MSM entry on the calling thread's device since nwc_init: passed (their votes'
- * bits set by the equation), failed (re-decided by the sub-batches), of the failed ones, groups with
+ * bits set by the equation), failed (re-decided by the leaves), of the failed ones, groups with
  * more distinct keys than the LDS key table holds (126), and groups the skip policy handed to the
- * sub-batches without the equation.  Any pointer may be null.  Waits for the device.  Diagnostics
+ * leaves without the equation.  Any pointer may be null.  Waits for the device.  Diagnostics
  * only. */
 int nwc_msm_stats(uint64_t* groups_passed, uint64_t* groups_failed, uint64_t* key_overflows, uint64_t* groups_skipped);
 int nwc_dev_sha512_trunc32(const void* d_data, const void* d_offsets, uint64_t n, void* d_out32,

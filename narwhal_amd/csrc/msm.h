@@ -29,10 +29,11 @@
 //   phase 3: - (sum z_i s_i mod l) B from the radix-2^22 basepoint comb, the identity test.
 //
 // A group that passes sets its votes' leaf bits; one that fails -- a vote that does not parse or
-// decode, more than MSM_KMAX distinct keys, or the equation -- lists its votes for the Straus
-// sub-batches (list-mode k_verify_straus), whose failing sub-batches go to the exact per-vote
-// leaves.  Semantics are the Straus entry's: exact on the deterministic
-// domain, dalek's acceptance probabilities on the randomized one.
+// decode, more than MSM_KMAX distinct keys, or the equation -- lists its votes for the exact
+// per-vote leaves (list-mode k_verify), never for a second random equation.  Semantics (DESIGN.md
+// §2.3, §4.2e): exact on the deterministic domain; on the randomized one a vote passes iff its
+// group's equation holds.  The entry takes this path only when no key combs apply: otherwise it
+// runs the comb leaves and dalek's equation per certificate (resolve.h).
 #pragma once
 
 namespace nwc {
@@ -75,13 +76,16 @@ enum : int {
   MSM_ST_MODE = 3,      // 0: the equation on every group; k = 1 .. MSM_SKIP_LAUNCHES - 1: on none (k-th such launch)
   MSM_ST_RUN = 4,       // this launch: groups the equation ran on
   MSM_ST_RUN_FAILED = 5,// this launch: of them, failed
-  MSM_ST_SKIPPED = 6,   // groups handed to the Straus sub-batches without the equation (cumulative)
+  MSM_ST_SKIPPED = 6,   // groups handed to the leaves without the equation (cumulative)
   MSM_ST_WORDS = 8
 };
 // When more than half of a launch's groups fail (a bad-vote rate of ~1/group or more: every group
 // holds one), the next MSM_SKIP_LAUNCHES - 1 launches skip the equation and pass every vote
-// straight to the Straus sub-batches (which a failing group's votes reach anyway, after a wasted
-// MSM); the launch after them runs it on every group again to re-measure.  Skipping within a
+// straight to the leaves (which a failing group's votes reach anyway, after a wasted MSM); the
+// launch after them runs it on every group again to re-measure.  The state is per device (one
+// set of words in DevCtx::msm_stats), shared by every caller and stream: one caller's bad launch
+// makes the next launches of any caller skip the equation -- their verdicts are unchanged (the
+// leaves are exact), only their speed (tests/test_gpu_msm.py).  Skipping within a
 // launch would not help: a wave's group is latency-bound (one group alone takes as long as a full
 // launch, profiles/r05/msm.md), so any probe costs a whole MSM launch -- 1 in 8 amortises it.
 constexpr u32 MSM_SKIP_LAUNCHES = 8;

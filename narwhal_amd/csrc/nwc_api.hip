@@ -247,9 +247,6 @@ struct DevCtx {
 #ifndef NWC_HOST_CHUNK_GROWTH
 #define NWC_HOST_CHUNK_GROWTH 3
 #endif
-#ifndef NWC_LEAF_ROUNDS
-#define NWC_LEAF_ROUNDS 0   // nwc_sanitize_messages from host memory: leaf launch granularity (A/B: profiles/r05/wire_host.md)
-#endif
 #ifndef NWC_PINNED_STAGE_MAX
 #define NWC_PINNED_STAGE_MAX (1u << 20)
 #endif
@@ -716,8 +713,9 @@ int lk_ensure(DevCtx& d, hipStream_t s) {
   HIP_TRY(hipMalloc(&k.slots, 4 * (size_t)nwc::LK_SLOTS));
   HIP_TRY(hipMalloc(&k.bases, (size_t)nwc::LK_MAX_KEYS * nwc::KeyComb::windows * sizeof(nwc::ge_p3)));
   HIP_TRY(hipMalloc(&k.state, 16));
-  if (!d.lk_demand) {
-    HIP_TRY(hipHostMalloc(&d.lk_demand, sizeof(uint32_t), hipHostMallocCoherent));
+  if (!d.lk_demand) HIP_TRY(hipHostMalloc(&d.lk_demand, sizeof(uint32_t), hipHostMallocCoherent));
+  {
+    // (again after nwc_trim, which resets the set's struct but keeps this word)
     void* dp = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dp, d.lk_demand, 0));
     k.host_demand = static_cast<uint32_t*>(dp);
@@ -732,16 +730,19 @@ int lk_ensure(DevCtx& d, hipStream_t s) {
   return 0;
 }
 
-// Room for the keys that asked to join: the first launch-key launch runs the census once and waits
-// for its demand; later launches read the demand the previous ones left in host memory (no sync)
-// and grow the combs stream-ordered on s (held combs copied), so a key that did not fit joins at
-// the next launch.  Called after s waits for scratch_free (no launch still reads the set).
+// Room for the keys that asked to join: the first launch-key launch (and the first after
+// nwc_set_committee emptied the set) runs the census once and waits for its demand; later launches
+// read the demand the previous ones left in host memory (no sync) and grow the combs
+// stream-ordered on s (held combs copied), so a key that did not fit joins at the next launch.
+// Called after s waits for scratch_free (no launch still reads the set).
 int lk_reserve(DevCtx& d, const uint8_t* pks, uint64_t n, hipStream_t s) {
   nwc::LaunchKeys& k = d.lk;
   if (k.cap >= nwc::LK_MAX_KEYS) return 0;
   if (!d.lk_censused) {
-    // cap 0 and nothing held: the select only counts (no key joins), then the host reads its demand
-    hipLaunchKernelGGL(nwc::k_lk_select, dim3(1), dim3(1024), 0, s, pks, n, k);
+    // nothing held: with the room for no key the select only counts, then the host reads its demand
+    nwc::LaunchKeys count_only = k;
+    count_only.cap = 0;
+    hipLaunchKernelGGL(nwc::k_lk_select, dim3(1), dim3(1024), 0, s, pks, n, count_only);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     d.lk_censused = true;
@@ -761,15 +762,9 @@ int lk_reserve(DevCtx& d, const uint8_t* pks, uint64_t n, hipStream_t s) {
   return 0;
 }
 
-// NWC_HOST_STAGING=0: large host calls copy straight from pageable memory (A/B); otherwise through
-// the device's pinned stages, filled by NWC_HOST_STAGING_THREADS (8) host threads.
-bool host_staging() {
-  static const bool on = [] {
-    const char* e = std::getenv("NWC_HOST_STAGING");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  return on;
-}
+// Large host calls copy their pageable inputs through the device's pinned stages, filled by
+// NWC_HOST_STAGING_THREADS (8) host threads (straight from pageable memory measured 7-10 % slower,
+// profiles/r05/wire_host.md; that switch was removed in round 6).
 // NWC_HOST_TIMING: per-phase times of large host calls on stderr (diagnostics)
 bool host_timing() {
   static const bool on = std::getenv("NWC_HOST_TIMING") != nullptr;
@@ -783,10 +778,10 @@ unsigned stager_threads() {
   return t;
 }
 
-// The device's transfer stream and (NWC_HOST_STAGING) its pinned stages.  Caller holds d.mu.
+// The device's transfer stream and its pinned stages.  Caller holds d.mu.
 int ensure_stager(DevCtx& d) {
   if (!d.xfer) HIP_TRY(hipStreamCreateWithFlags(&d.xfer, hipStreamNonBlocking));
-  if (!d.stager && host_staging()) {
+  if (!d.stager) {
     auto st = std::make_unique<HostStager>();
     const hipError_t e = st->init(d.xfer, stager_threads());
     if (e != hipSuccess) {
@@ -1297,13 +1292,12 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     // chunk k verifies (~100 M/s), so it arrives in time while growing up to ~3.7x; fewer, larger
     // launches leave fewer kernel tails (the first chunk is one round of resident lanes).
     if (int rc = ensure_stager(d)) return rc;
-    // copies of one chunk's inputs: through the pinned stages, or straight from pageable memory
-    HostStager* const hs = host_staging() ? d.stager.get() : nullptr;
-    if (hs) hs->reset();
+    // copies of one chunk's inputs: through the pinned stages
+    HostStager* const hs = d.stager.get();
+    hs->reset();
     const auto tv0 = std::chrono::steady_clock::now();
     auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
-      if (hs) return hs->put(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), bytes);
-      return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d.xfer);
+      return hs->put(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), bytes);
     };
     std::vector<uint64_t> cuts{0};
     // chunks stop growing at NWC_HOST_CHUNK_MAX equations: when the kernels keep pace with the
@@ -1332,7 +1326,7 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
       // event (recorded later on the same stream) covers it
       HIP_TRY(h2d(dm, msgs, msg_bytes));
       HIP_TRY(h2d(doffs, cert_offsets + c_lo, offs_bytes));
-      if (hs) HIP_TRY(hs->flush());
+      HIP_TRY(hs->flush());
       launch_cert_index(doffs, c_lo, c_end, lo, hi, dmi, d.xfer);
       HIP_TRY(hipGetLastError());
     } else if (!msg_stride) {
@@ -1343,7 +1337,7 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
       if (msg_stride) HIP_TRY(h2d(dm + 32 * c0, msgs + 32 * (lo + c0), 32 * len));
       HIP_TRY(h2d(dp + 32 * c0, pks + 32 * (lo + c0), 32 * len));
       HIP_TRY(h2d(ds + 64 * c0, sigs + 64 * (lo + c0), 64 * len));
-      if (hs) HIP_TRY(hs->flush());
+      HIP_TRY(hs->flush());
       HIP_TRY(hipEventRecord(d.ev_chunk[k], d.xfer));
       HIP_TRY(hipStreamWaitEvent(d.stream, d.ev_chunk[k], 0));
       if (int rc = launch_verify(d, msg_stride ? dm + 32 * c0 : dm, batch ? dmi + c0 : nullptr, msg_stride ? 1 : 0,
@@ -2000,9 +1994,10 @@ static int set_committee_locked(const uint8_t* pks, size_t n) {
     HIP_TRY(hipEventSynchronize(d.scratch_free));   // no verify launch still reads the old cache
     HIP_TRY(hipStreamSynchronize(d.stream));
     auto_reset(d);   // keys remembered under the old committee are stale
-    if (d.lk_alloc) {   // so are the launch keys
+    if (d.lk_alloc) {   // so are the launch keys (the next launch-key launch measures its demand anew)
       HIP_TRY(hipMemsetAsync(d.lk.slots, 0xFF, 4 * (size_t)nwc::LK_SLOTS, d.stream));
       HIP_TRY(hipMemsetAsync(d.lk.state, 0, 16, d.stream));
+      d.lk_censused = false;
     }
     if (d.cm_keys) HIP_TRY(hipFree(d.cm_keys));
     if (d.cm_flags) HIP_TRY(hipFree(d.cm_flags));
@@ -2356,8 +2351,10 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
 // `chunk_queued(k)` tells without waiting whether they are, and chunk k's parse is then queued
 // before the host waits for chunk k - 1's count.  The chunks share one vote-slot counter, so the
 // votes of the chunks parsed so far are contiguous; after each parse the host reads the count and
-// launches those votes' leaves (NWC_LEAF_ROUNDS: in whole rounds of the leaf kernel's resident
-// lanes) on the side stream beside the next chunk's parse, and the rest after the last chunk.
+// launches those votes' leaves on the side stream beside the next chunk's parse, and the rest
+// after the last chunk.  (Measured and removed in round 6: leaves behind the parses on one stream,
+// leaves in whole comb rounds, per-launch list passes, each parse queued only after the previous
+// count -- profiles/r05/wire_host.md, ab_wire_modes.txt, ab_wire_defer_lists.txt.)
 // The strict equations (headers' and votes' own signatures) of all chunks but the last run while
 // the last one crosses PCIe; the header digests and the final codes run once over all m messages.
 static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, size_t m, uint64_t total,
@@ -2422,22 +2419,13 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   // the leaf stream when chunks overlap: the side stream, which has a hardware queue of its own
   // (GPU_MAX_HW_QUEUES = 4: a stream created later shared the transfer stream's queue, and its
   // leaves waited behind the markers of the in-flight copies, profiles/r05/wire_host.md)
-  // NWC_LEAF_STREAM=0: the leaves on s behind the parses (no overlap of the two, A/B)
-  static const bool leaf_side = [] {
-    const char* e = std::getenv("NWC_LEAF_STREAM");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
   const bool chunked = nch > 1;
-  const hipStream_t ls = chunked && leaf_side ? d.side : s;
+  const hipStream_t ls = chunked ? d.side : s;
   // the leaf launches of a chunked call on the committee-cache comb path only list their uncached
   // equations (LV_DEFER_LIST); the list's half-size, fallback and torsion passes run once, after
   // the leaves queued before the first strict launch (which reuses the list), instead of ~8 small
-  // launches per chunk on the leaf stream (NWC_DEFER_LISTS=0: per launch, A/B)
-  static const bool defer_env = [] {
-    const char* e = std::getenv("NWC_DEFER_LISTS");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  const bool defer = chunked && defer_env && deferrable_list(d);
+  // launches per chunk on the leaf stream
+  const bool defer = chunked && deferrable_list(d);
   struct HoldLists {
     DevCtx& d;
     ~HoldLists() { d.hold_lists = false; }
@@ -2461,13 +2449,6 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   auto mark = [&](const char* what) {
     if (timing) marks.emplace_back(what, std::chrono::duration<double>(std::chrono::steady_clock::now() - tm0).count() * 1e3);
   };
-  // leaf launches in units of `leaf_rounds` rounds of the leaf kernel's resident lanes (the
-  // committee comb kernel's: one equation per lane a round); 0 = one launch per chunk
-  static const uint64_t leaf_rounds = [] {
-    const char* e = std::getenv("NWC_LEAF_ROUNDS");
-    return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)NWC_LEAF_ROUNDS;
-  }();
-  const uint64_t round = leaf_rounds ? std::max<uint64_t>(64, leaf_rounds * d.cus * d.comb_blocks_per_cu * 256) : 64;
   uint64_t launched = 0;   // votes [0, launched) have their leaf launch queued
   auto leaves = [&](uint64_t upto, bool deferred) -> int {
     if (upto <= launched) return 0;
@@ -2527,18 +2508,15 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     if (queued < nch && (!chunk_queued || chunk_queued(queued)))
       if (int rc = queue_parse()) return rc;
     if (!chunked) continue;
-    // the votes parsed so far, in whole rounds, on the leaf stream; the next chunk's copy goes
-    // on in the copier thread meanwhile, and its parse runs beside these leaves
+    // the votes parsed so far on the leaf stream; the next chunk's copy goes on in the copier
+    // thread meanwhile, and its parse runs beside these leaves
     HIP_TRY(hipEventSynchronize(d.ev_cnt[k]));
     nv = std::min<uint64_t>(nv_host[k], vt);
     mark("count");
-    if (ls != s) HIP_TRY(hipStreamWaitEvent(ls, d.ev_cnt[k], 0));
-    // (before the last chunk every vote so far: the last leaf launch then holds only the last
-    // chunk's votes)
-    if (k + 2 == nch || (k + 1 < nch && !leaf_rounds))
+    HIP_TRY(hipStreamWaitEvent(ls, d.ev_cnt[k], 0));
+    // (the last leaf launch then holds only the last chunk's votes)
+    if (k + 1 < nch)
       if (int rc = leaves(nv, defer)) return rc;
-    if (k + 2 < nch && leaf_rounds)
-      if (int rc = leaves(launched + (nv - launched) / round * round, defer)) return rc;
     // the strict equations of every chunk but the last while the last one crosses PCIe
     // (cuts[nch - 1] is a multiple of 64 messages: the two strict launches own their words)
     if (k + 2 == nch) {
@@ -2558,10 +2536,8 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
                                sbits + c0 / 64, ls))
       return rc;
     if (int rc = leaves(nv, false)) return rc;
-    if (ls != s) {
-      HIP_TRY(hipEventRecord(d.ev_msg, ls));
-      HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
-    }
+    HIP_TRY(hipEventRecord(d.ev_msg, ls));
+    HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
   } else {
     // one chunk: the strict launch (it needs no count) queued before the host waits for the
     // count, the Header::digest checks beside the leaves on the side stream
@@ -2625,7 +2601,7 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
   uint8_t* ddig = digests32 ? c.take<uint8_t>(32 * m) : nullptr;
   std::vector<uint64_t> hoff(m + 1);
   for (size_t i = 0; i <= m; ++i) hoff[i] = offsets[i] - base;
-  const bool staged = host_staging() && total >= ((size_t)4 << 20);
+  const bool staged = total >= ((size_t)4 << 20);
   // Large batches (config 3 from the wire: 10 KB per certificate) go through the pinned stages on
   // the transfer stream in chunks of ~NWC_MSG_CHUNK bytes cut on message boundaries; chunk k is
   // parsed and verified while chunk k + 1 crosses PCIe.  The chunks share the message offsets
@@ -2719,13 +2695,7 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
       if (e != hipSuccess) return set_err(NWC_ERR_DEVICE, "hipStreamWaitEvent: %s", hipGetErrorString(e));
       return 0;
     };
-    // NWC_PARSE_AHEAD=0: each chunk's parse queued only after the previous chunk's count (A/B)
-    static const bool parse_ahead = [] {
-      const char* e = std::getenv("NWC_PARSE_AHEAD");
-      return !(e && std::strcmp(e, "0") == 0);
-    }();
     auto chunk_queued = [&](size_t k) -> bool {
-      if (!parse_ahead) return false;
       std::lock_guard<std::mutex> g(cmu);
       return recorded > k;
     };

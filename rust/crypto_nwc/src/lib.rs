@@ -77,10 +77,13 @@ pub fn verify_batch(digest: &[u8; 32], public_keys: &[[u8; 32]], signatures: &[[
 
 /// Many certificates at once (certificate c = `digests[c]` over votes `offsets[c]..offsets[c+1]`):
 /// per-certificate verdicts and the bad-vote set.  `dalek_batch = false`: the exact per-vote leaves
-/// (deterministic; Err on dalek's randomized domain); `true`: dalek's own random-linear-combination
-/// equation as a Pippenger MSM per group of votes, groups that fail re-decided by sub-batches of
-/// ~12 votes and those by the leaves (3.5x the leaves on clean traffic without a key cache; dalek's
-/// probabilities on the randomized domain).  Returns (certificate ok, vote bad) as bitmaps.
+/// (deterministic; Err on dalek's randomized domain); `true`: dalek's batch semantics -- each
+/// certificate passes iff dalek's random-linear-combination equation holds for it: the comb-path
+/// leaves for every vote, then the equation once per certificate over the votes they rejected
+/// (exact in the 8-torsion group; the committee's repeated keys give the comb path without
+/// `set_committee`), or, where no key combs apply, a Pippenger MSM per group of votes with the
+/// leaves for the groups it rejects.  Each vote meets at most one random equation.  Returns
+/// (certificate ok, vote bad) as bitmaps.
 pub fn verify_batch_many(digests: &[[u8; 32]], offsets: &[u32], public_keys: &[[u8; 32]], signatures: &[[u8; 64]],
                          dalek_batch: bool) -> (Vec<u8>, Vec<u8>) {
     let m = digests.len();

@@ -89,8 +89,13 @@ def test_set_fills_and_other_committees_take_the_ladder(oracle):
     both = tuple(a[perm] for a in both)
     exp = oracle.leaf_many(*both)
     got = _leaf(*both)
+    # the combs have room for the 120 held keys: this launch records the demand (128) ...
+    assert _held(lib)[0] == 120
+    got2 = _leaf(*both)
+    # ... and the next one grows them first: 8 more join, the set is full
     assert _held(lib)[0] == 128
-    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    for g in (got, got2):
+        assert (g == exp).all(), np.nonzero(g != exp)[0][:10]
     _lib.check(lib.nwc_set_committee(None, 0))
     assert _held(lib)[0] == 0
 

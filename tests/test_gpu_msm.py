@@ -285,3 +285,39 @@ def test_key_table_capacity_boundary(oracle, nkeys):
         assert (s1[0] - s0[0], s1[1] - s0[1], s1[2] - s0[2]) == (1, 0, 0), (s0, s1)
     else:
         assert (s1[0] - s0[0], s1[1] - s0[1], s1[2] - s0[2]) == (0, 1, 1), (s0, s1)
+
+
+def test_skip_policy_is_device_wide_and_verdicts_hold(oracle):
+    """The skip policy's state is per device (include/nwc.h): one caller's high-bad-rate launch on
+    its stream makes the next launch of another caller, on another stream with clean traffic, skip
+    the equation (its groups go straight to the leaves) -- slower for it, with the same verdicts."""
+    import torch
+    from narwhal_amd import _lib, device
+    _lib.diag_set("msm_adapt", 1)
+    _lib.diag_set("msm_group", 512)
+    try:
+        rng = np.random.default_rng(63)
+        bdig, boffs, bpks, bsigs, _ = _committee_certs(oracle, rng, 200, bad_rate=0.03)
+        cdig, coffs, cpks, csigs, _ = _committee_certs(oracle, rng, 200)
+        ocert, obad = oracle.batch_many(bdig, boffs.astype(np.uint32), bpks, bsigs)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        # the bad caller measures (the policy's re-measuring launch), fails its groups and arms the skip
+        for _ in range(8):
+            s0 = device.msm_stats()
+            with torch.cuda.stream(s1):
+                cert, bad = _run(bdig, boffs, bpks, bsigs)
+            s1.synchronize()
+            if device.msm_stats()[1] > s0[1]:
+                break
+        assert (cert == ocert).all() and (bad == obad).all()
+        st0 = device.msm_stats()
+        with torch.cuda.stream(s2):
+            cert, bad = _run(cdig, coffs, cpks, csigs)
+        s2.synchronize()
+        st1 = device.msm_stats()
+        assert cert.all() and not bad.any()
+        groups = (int(coffs[-1]) + 511) // 512
+        assert (st1[0] - st0[0], st1[3] - st0[3]) == (0, groups), (st0, st1)
+    finally:
+        _lib.diag_set("msm_group", 0)
+        _lib.diag_set("msm_adapt", 0)
