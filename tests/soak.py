@@ -13,6 +13,11 @@ their votes with the comb kernel, the rest with the ladder.
 
 --call C verifies each chunk in device calls of at most C equations (C <= 1024 without a
 committee: the cold kernel, k_verify_cold, one block per equation).
+--dalek runs every chunk, cut into ragged certificates as --host-batch does, through the MSM
+entry with dalek's batch semantics (nwc_dev_verify_batch_msm: with launch keys, the comb leaves and
+dalek's equation per certificate over their failing votes, resolve.h) with the z seed fixed, and
+compares every certificate bit with the oracle's evaluation of dalek's equation for the same z_i
+(orc_batch_z8) and the bad-vote bits with the leaves of the failing certificates.
 --straus also runs every chunk through dalek's batch equation over sub-batches
 (nwc_dev_verify_batch_straus, each triple its own certificate, so sub-batches mix every class):
 its per-vote bits must equal the oracle leaf on every vote outside dalek's randomized domain
@@ -97,6 +102,8 @@ def main():
                     help="also nwc_verify_batch_many from host memory: each chunk's triples in ragged certificates "
                          "(0..130 votes, votes signing their certificate's digest before mutation), certificate and "
                          "bad-vote bits vs the oracle's batch_many on the same inputs")
+    ap.add_argument("--dalek", action="store_true",
+                    help="also the per-certificate dalek equation (fixed seed) on ragged certificates vs orc_batch_z8")
     ap.add_argument("--valid-frac", type=float, default=0.30,
                     help="share of unmutated triples (0.99: most Straus sub-batches pass, the rest exercise the leaves)")
     args = ap.parse_args()
@@ -119,6 +126,8 @@ def main():
     stats = {c: {"n": 0, "strict_valid": 0, "leaf_valid": 0, "strict_mismatch": 0, "leaf_mismatch": 0,
                  "straus_mismatch": 0, "randomized": 0, "straus_randomized_pass": 0} for c in CLASSES}
     host_batch = {"votes": 0, "certificates": 0, "bad_votes": 0, "failing_certificates": 0, "mismatch": 0}
+    dalek = {"votes": 0, "certificates": 0, "failing_certificates": 0, "certificates_with_randomized_votes": 0,
+             "randomized_certificates_passed": 0, "mismatch": 0}
     t0 = time.time()
     done = 0
     mism = []
@@ -132,7 +141,7 @@ def main():
             seeds = lseeds[who]
         else:
             seeds = device.derive32(b"soak-seed", done, n)
-        if args.host_batch:
+        if args.host_batch or args.dalek:
             # ragged certificates over this chunk's triples; vote v signs its certificate's digest
             counts = []
             while sum(counts) < n:
@@ -183,6 +192,45 @@ def main():
             host_batch["bad_votes"] += int(obad.sum())
             host_batch["failing_certificates"] += int((~ocert.astype(bool)).sum())
             host_batch["mismatch"] += hb_mis
+        if args.dalek:
+            import hashlib
+            from concurrent.futures import ThreadPoolExecutor
+            seed = 0x5EED0000 + done // args.chunk
+            _lib.diag_set("dalek_seed", seed)
+            try:
+                do = torch.from_numpy(offs.astype(np.int32)).cuda()
+                dmi = torch.from_numpy(vote_cert.astype(np.int32)).cuda()
+                leafw = device.verify_batch_msm(torch.from_numpy(cdig).cuda(), do, dmi, tp, ts)
+                cw, bw = device.cert_reduce(leafw, do, n)
+                torch.cuda.synchronize()
+            finally:
+                _lib.diag_set("dalek_seed", 0)
+            gcert, gbad = device.unpack_bits(cw, ncert), device.unpack_bits(bw, n)
+            sb = seed.to_bytes(4, "little") + bytes(28)
+            zs = np.frombuffer(b"".join(hashlib.sha512(sb + v.to_bytes(8, "little")).digest()[:16] for v in range(n)),
+                               np.uint8).reshape(n, 16)
+            parts = np.array_split(np.arange(ncert), threads)
+
+            def z8(part):
+                if len(part) == 0:
+                    return np.zeros(0, bool)
+                c0, c1 = int(part[0]), int(part[-1]) + 1
+                v0, v1 = int(offs[c0]), int(offs[c1])
+                return orc.batch_z_many(cdig[c0:c1], (offs[c0:c1 + 1] - v0).astype(np.uint32), p[v0:v1], s[v0:v1],
+                                        zs[v0:v1], z8=True)
+            with ThreadPoolExecutor(threads) as ex:
+                ocert = np.concatenate(list(ex.map(z8, parts)))
+            obad = ~ol.astype(bool) & ~np.repeat(ocert, counts)
+            dmis = int((gcert != ocert).sum()) + int((gbad != obad).sum())
+            cls = orc.vote_class_many(m, p, s, threads=threads)
+            csum = np.concatenate([[0], np.cumsum(cls == 1)])
+            rcert = (csum[offs[1:].astype(np.int64)] - csum[offs[:-1].astype(np.int64)]) > 0
+            dalek["votes"] += n
+            dalek["certificates"] += ncert
+            dalek["failing_certificates"] += int((~ocert).sum())
+            dalek["certificates_with_randomized_votes"] += int(rcert.sum())
+            dalek["randomized_certificates_passed"] += int((rcert & ocert).sum())
+            dalek["mismatch"] += dmis
         for j in np.nonzero((gs != os_) | (gl != ol) | smis)[0][:20]:
             mism.append({"class": CLASSES[kind[j]], "index": int(done + j), "msg": m[j].tobytes().hex(),
                          "pk": p[j].tobytes().hex(), "sig": s[j].tobytes().hex(), "gpu_strict": bool(gs[j]),
@@ -211,13 +259,14 @@ def main():
         held = h.value
     out = {"triples": args.n, "committee": args.committee, "launch_keys": args.launch_keys, "launch_keys_held": held,
            "call": args.call, "straus": args.straus, "host_batch": host_batch if args.host_batch else None,
+           "dalek": dalek if args.dalek else None,
            "valid_frac": args.valid_frac, "oracle_threads": threads, "seconds": time.time() - t0, "classes": stats, "total": total,
            "mismatches": mism}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(out, open(args.out, "w"), indent=1)
-    print(json.dumps(dict(total, host_batch_mismatch=host_batch["mismatch"])))
+    print(json.dumps(dict(total, host_batch_mismatch=host_batch["mismatch"], dalek_mismatch=dalek["mismatch"])))
     return 0 if (total["strict_mismatch"] == 0 and total["leaf_mismatch"] == 0 and total["straus_mismatch"] == 0
-                 and host_batch["mismatch"] == 0) else 1
+                 and host_batch["mismatch"] == 0 and dalek["mismatch"] == 0) else 1
 
 
 if __name__ == "__main__":
