@@ -1130,41 +1130,6 @@ struct CombArgs {
   uint32_t list_base;              // added to the equation index a comb kernel lists (a call-wide list
                                    // over consecutive launches, nwc_api.hip LV_DEFER_LIST)
 };
-// k_verify_stream's extra argument: the inputs are in pinned host memory that host threads fill
-// while the kernel runs; slice s (equations [s slice, (s + 1) slice)) may be read once
-// ready[s] != 0.  A wave that waits too long sets *err and the launch stops.  (Its own struct, so
-// the headline kernel's argument block is unchanged.)
-struct StreamArgs {
-  const uint32_t* ready;
-  uint32_t slice;
-  uint32_t* err;
-};
-
-// STREAM launches: wait until the wave's equations [b0, b0 + 64) have been copied in (lane 0 polls
-// the host-written flag, relaxed at system scope, with s_sleep between polls), then an agent-scope
-// acquire so no input load moves above the poll.  Bounded: ~1 s, then the error word is set.
-// Returns false when the launch is stopping (an error flagged by any wave).
-__device__ __forceinline__ bool stream_wait(const StreamArgs& sa, uint64_t b0) {
-  bool ok = true;
-  if ((threadIdx.x & 63u) == 0) {
-    if (__hip_atomic_load(sa.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      ok = false;
-    } else {
-      const uint32_t* flag = sa.ready + (uint32_t)(b0 / sa.slice);
-      for (uint32_t it = 0; !__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); ++it) {
-        if (it > (1u << 20)) {
-          atomicOr(sa.err, 1u);
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(32);
-      }
-    }
-  }
-  ok = __shfl(ok, 0, 64);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return ok;
-}
 
 __device__ __forceinline__ void load_inputs(const VerifyArgs& a, uint64_t i, u32 mw[8], u32 aw[8], u32 sgw[16]) {
   const uint64_t mi = a.msg_index ? (uint64_t)a.msg_index[i] : i * a.msg_stride;
@@ -1242,42 +1207,6 @@ __global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify(Verif
       w[0] = t_entry; w[1] = t_exit; w[2] = r_entry; w[3] = r_exit;
     }
   }
-}
-
-// The strict half-size kernel over inputs that host threads copy into pinned host memory while it
-// runs (StreamArgs; nwc_api.hip verify_range, LV_STREAM): k_verify<true, false>'s tile loop with a
-// bounded wait for the tile's slice in front of its input loads.  A kernel of its own, so the
-// headline k_verify's code stays exactly as it is.
-__global__ __launch_bounds__(256, NWC_VERIFY_WAVES_PER_SIMD) void k_verify_stream(VerifyArgs a, CombArgs ca, StreamArgs sa) {
-  __shared__ uint4 lds[4 * STAGE_U4_PER_WAVE + BASE_DIGIT_WORDS * 64];
-  uint4* stage = lds + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * STAGE_U4_PER_WAVE;
-  const BaseDigits bd{reinterpret_cast<i32*>(lds + 4 * STAGE_U4_PER_WAVE) + threadIdx.x};
-  const uint64_t n = a.n;
-  const u32 lane = threadIdx.x & 63u;
-  const size_t slot = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint8_t* base = a.scratch + slot * 2 * TAB_BYTES_PER_LANE;
-  const LaneTable ta{reinterpret_cast<uint4*>(base)};
-  const LaneTable tr{reinterpret_cast<uint4*>(base + TAB_BYTES_PER_LANE)};
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t bb = (uint64_t)blockIdx.x * blockDim.x; bb < n; bb += stride) {
-    const uint64_t b0 = bb + (threadIdx.x & ~63u);   // this wave's 64 equations
-    const u32 tile = (u32)(b0 >> 6);
-    const uint64_t i = b0 + lane;
-    const bool active = i < n;
-    if (!stream_wait(sa, b0 < n ? b0 : n - 1)) break;   // wave-uniform: the launch is stopping
-    u32 mw[8], aw[8], sgw[16];
-    load_inputs(a, active ? i : 0, mw, aw, sgw);
-    bool fb = false;
-    bool v = verify_half<false>(mw, aw, sgw, a.strict != 0, a.base24, stage, bd, ta, tr, a.committee, fb,
-                                (int)a.force_windows);
-    if (a.force_fb_every && (i % a.force_fb_every) == 0) { fb = true; v = false; }
-    v = v && active;
-    fb = fb && active;
-    if (fb) a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)i;
-    const uint64_t ballot = __ballot(v);
-    if (lane == 0 && b0 < n) a.out_bits[tile] = ballot;
-  }
-  (void)ca;
 }
 
 template __global__ void k_verify<true, false>(VerifyArgs, CombArgs);

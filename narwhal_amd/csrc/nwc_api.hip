@@ -173,14 +173,6 @@ struct DevCtx {
   uint32_t cc_n = 0;
   uint8_t* msg_arena = nullptr;   // nwc_sanitize_messages buffers
   size_t msg_arena_cap = 0;
-  // large strict host calls with streamed inputs (verify_range): pinned, host-coherent input
-  // arrays the kernel reads in place while host threads fill them, one ready flag per slice
-  uint8_t* zin = nullptr;
-  uint8_t* zin_dev = nullptr;
-  size_t zin_cap = 0;
-  uint32_t* zs_err = nullptr;          // device word: a streamed launch gave up waiting
-  const uint32_t* zs_ready = nullptr;  // set by verify_range around its LV_STREAM launch
-  uint32_t zs_slice = 0;
   uint8_t* pinned = nullptr;   // host staging for small calls: one H2D and one D2H per call, or
   uint8_t* pinned_dev = nullptr;   // read in place by the latency kernel through this device pointer
   size_t pinned_cap = 0;
@@ -210,16 +202,6 @@ struct DevCtx {
   std::unique_ptr<HostStager> stager;
   std::mutex mu;
 
-  int ensure_zin(size_t bytes) {
-    if (bytes <= zin_cap) return 0;
-    if (zin) { (void)hipHostFree(zin); zin = nullptr; zin_cap = 0; }
-    HIP_TRY(hipHostMalloc(&zin, bytes, hipHostMallocCoherent));
-    void* dp = nullptr;
-    HIP_TRY(hipHostGetDevicePointer(&dp, zin, 0));
-    zin_dev = static_cast<uint8_t*>(dp);
-    zin_cap = bytes;
-    return 0;
-  }
   int ensure_pinned(size_t bytes) {
     if (bytes <= pinned_cap) return 0;
     if (pinned) { (void)hipHostFree(pinned); pinned = nullptr; pinned_cap = 0; }
@@ -348,7 +330,6 @@ int init_device(DevCtx& d) {
   d.comb_blocks_per_cu = bpc > 0 ? bpc : 1;
   HIP_TRY(hipMalloc(&d.uc_count, sizeof(uint32_t)));
   HIP_TRY(hipMalloc(&d.fb_count, sizeof(uint32_t)));
-  HIP_TRY(hipMalloc(&d.zs_err, sizeof(uint32_t)));
   HIP_TRY(hipStreamSynchronize(d.stream));
   return 0;
 }
@@ -784,17 +765,6 @@ int lk_reserve(DevCtx& d, const uint8_t* pks, uint64_t n, hipStream_t s) {
 // Large host calls copy their pageable inputs through the device's pinned stages, filled by
 // NWC_HOST_STAGING_THREADS (8) host threads (straight from pageable memory measured 7-10 % slower,
 // profiles/r05/wire_host.md; that switch was removed in round 6).
-// NWC_HOST_STREAM (default 1): large strict host calls stream their inputs into pinned host memory
-// the verification kernel reads in place (verify_range); 0 = the chunked DMA pipeline
-bool host_stream() {
-  static const bool on = [] {
-    const char* e = std::getenv("NWC_HOST_STREAM");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  return on;
-}
-constexpr uint64_t STREAM_SLICE = 16384;   // equations per ready flag (2 MB of inputs)
-
 // NWC_HOST_TIMING: per-phase times of large host calls on stderr (diagnostics)
 bool host_timing() {
   static const bool on = std::getenv("NWC_HOST_TIMING") != nullptr;
@@ -854,9 +824,7 @@ int release_idle_buffers(DevCtx& d, const uint8_t* in_use) {
 // count and sized the lists (ensure_scratch) for the whole call before the first such launch, and
 // runs the list, fallback and torsion passes once over all of them (finish_deferred_list).  The
 // chunked sanitize pipeline: one set of those small launches per call instead of per chunk.
-// LV_STREAM: the inputs are in d.zin, filled while the kernel runs; tile reads wait on
-// d.zs_ready (the strict half-size kernel only: no committee, not a cold-size launch, one launch)
-constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4, LV_STAMP = 8, LV_DEFER_LIST = 16, LV_STREAM = 32;
+constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4, LV_STAMP = 8, LV_DEFER_LIST = 16;
 
 // launch_verify's comb path over the committee cache for any n (what LV_DEFER_LIST needs)
 bool deferrable_list(const DevCtx& d) {
@@ -979,11 +947,6 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   a.force_windows = knobs().force_windows.load();
   a.stamps = d.stamps;
   const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16, nullptr, (uint32_t)(defer ? list_base : 0)};
-  const bool streamed = (flags & LV_STREAM) != 0;
-  if (streamed && (!d.zs_ready || !strict || comb || cm.n || path != VPath::Default || n <= cold_max() ||
-                   n > verify_max_launch()))
-    return set_err(NWC_ERR_ARG, "streamed launch off the strict half-size path");
-  const nwc::StreamArgs sa{d.zs_ready, d.zs_slice, d.zs_err};
   const bool half = path != VPath::Full;
   // small batch-leaf launches outside the comb path: the keys' torsion test (one long serial
   // lane per new key) runs on the side stream beside the verification instead of after it
@@ -1032,8 +995,6 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
       hipLaunchKernelGGL((nwc::k_verify<true, true>), dim3(grid), dim3(256), 0, s, a, ca);
     else if (half && (flags & LV_STAMP))
       hipLaunchKernelGGL((nwc::k_verify<true, false, false, true>), dim3(grid), dim3(256), 0, s, a, ca);
-    else if (half && streamed)
-      hipLaunchKernelGGL(nwc::k_verify_stream, dim3(grid), dim3(256), 0, s, a, ca, sa);
     else if (half)
       hipLaunchKernelGGL((nwc::k_verify<true, false>), dim3(grid), dim3(256), 0, s, a, ca);
     else
@@ -1320,57 +1281,6 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     const char* e = std::getenv("NWC_HOST_CHUNK");   // 0 = no pipelining (A/B)
     return e ? (uint64_t)std::strtoull(e, nullptr, 10) / 64 * 64 : (uint64_t)NWC_HOST_CHUNK;
   }();
-  if (!batch && msg_stride && host_stream() && n > cold_max() && n >= 2 * NWC_HOST_CHUNK && n <= verify_max_launch() &&
-      !d.cm_n && verify_path() == VPath::Default) {
-    // Streamed inputs (strict calls, BASELINE configs 2 and 5 from host memory): one launch of the
-    // strict kernel reads the triples in place from pinned host memory while the stager's host
-    // threads copy them there, slice by slice; a wave starts its tile once the tile's slice is
-    // flagged (bounded wait).  No DMA, no chunk launches and their tails: the kernel starts after
-    // the first slices (~2 MB) instead of the first 16-MB chunk, and runs as one long launch.
-    const uint64_t nsl = (n + STREAM_SLICE - 1) / STREAM_SLICE;
-    const size_t in_bytes = align256(128 * (size_t)n);
-    if (int rc = d.ensure_zin(in_bytes + 4 * nsl)) return rc;
-    if (int rc = ensure_stager(d)) return rc;
-    if (int rc = d.ensure_arena(align256(8 * (words + 1)))) return rc;
-    uint8_t* const hm = d.zin;
-    uint8_t* const hp = hm + 32 * n;
-    uint8_t* const hsg = hp + 32 * n;
-    uint32_t* const flags = reinterpret_cast<uint32_t*>(d.zin + in_bytes);
-    for (uint64_t k = 0; k < nsl; ++k) __atomic_store_n(&flags[k], 0u, __ATOMIC_RELAXED);
-    std::atomic_thread_fence(std::memory_order_seq_cst);
-    uint64_t* const dout = reinterpret_cast<uint64_t*>(d.arena);
-    HIP_TRY(hipMemsetAsync(d.zs_err, 0, sizeof(uint32_t), d.stream));
-    d.zs_ready = reinterpret_cast<const uint32_t*>(d.zin_dev + in_bytes);
-    d.zs_slice = (uint32_t)STREAM_SLICE;
-    const int lrc = launch_verify(d, d.zin_dev, nullptr, 1, d.zin_dev + 32 * n, d.zin_dev + 64 * n, n, strict, dout,
-                                  d.stream, LV_STREAM);
-    d.zs_ready = nullptr;
-    if (lrc) return lrc;   // nothing launched reads the inputs yet, or the launch already failed
-    // (no copy to pageable host memory may be queued before the slices are in: the runtime may
-    // perform it at enqueue, i.e. wait for the kernel, which waits for the slices)
-    // slices interleaved over the copy pool (slice s by thread s mod P), so the prefix the kernel
-    // reads first lands first; every flag written after its slice's bytes (release)
-    HostStager* const hs = d.stager.get();
-    const unsigned P = (unsigned)hs->pool.th.size() + 1;
-    const uint8_t* const sm = msgs + 32 * lo;
-    const uint8_t* const sp = pks + 32 * lo;
-    const uint8_t* const ss = sigs + 64 * lo;
-    hs->pool.run(P, [&](unsigned t) {
-      for (uint64_t k = t; k < nsl; k += P) {
-        const uint64_t e0 = k * STREAM_SLICE, e1 = std::min<uint64_t>(n, e0 + STREAM_SLICE);
-        std::memcpy(hm + 32 * e0, sm + 32 * e0, 32 * (e1 - e0));
-        std::memcpy(hp + 32 * e0, sp + 32 * e0, 32 * (e1 - e0));
-        std::memcpy(hsg + 64 * e0, ss + 64 * e0, 64 * (e1 - e0));
-        __atomic_store_n(&flags[k], 1u, __ATOMIC_RELEASE);
-      }
-    });
-    uint32_t err = 0;
-    HIP_TRY(hipMemcpyAsync(out_words.data(), dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
-    HIP_TRY(hipMemcpyAsync(&err, d.zs_err, sizeof err, hipMemcpyDeviceToHost, d.stream));
-    HIP_TRY(hipStreamSynchronize(d.stream));
-    if (err) return set_err(NWC_ERR_DEVICE, "streamed inputs: a wave gave up waiting for its slice");
-    return 0;
-  }
   static const uint64_t growth = [] {
     const char* e = std::getenv("NWC_HOST_CHUNK_GROWTH");   // 1 = equal chunks (A/B)
     return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : (uint64_t)NWC_HOST_CHUNK_GROWTH;
@@ -1902,8 +1812,6 @@ void nwc_shutdown(void) {
       (void)hipFree(d->lk.state);
     }
     if (d->pinned) (void)hipHostFree(d->pinned);
-    if (d->zin) (void)hipHostFree(d->zin);
-    if (d->zs_err) (void)hipFree(d->zs_err);
     if (d->cc_stakes) (void)hipFree(d->cc_stakes);
     if (d->cc_worker_off) (void)hipFree(d->cc_worker_off);
     if (d->cc_worker_ids) (void)hipFree(d->cc_worker_ids);
@@ -2892,8 +2800,6 @@ int nwc_trim(void) {
   d.rs_buf = nullptr; d.rs_cap = 0;
   if (d.arena) HIP_TRY(hipFree(d.arena));
   if (d.msg_arena) HIP_TRY(hipFree(d.msg_arena));
-  if (d.zin) HIP_TRY(hipHostFree(d.zin));
-  d.zin = nullptr; d.zin_dev = nullptr; d.zin_cap = 0;
   d.scratch = nullptr; d.scratch_cap = 0;
   d.straus_scratch = nullptr; d.straus_cap = 0;
   d.arena = nullptr; d.arena_cap = 0;

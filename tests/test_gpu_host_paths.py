@@ -34,27 +34,9 @@ def test_strict_many_host_chunks(oracle):
     assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
 
 
-def test_strict_many_host_dma_chunks():
-    """The same 400k-triple call through the chunked DMA pipeline (NWC_HOST_STREAM=0, read once per
-    process: a child), the path strict calls took before round 6 and batch calls still take; the
-    default streams the inputs into pinned memory the kernel reads in place (k_verify_stream)."""
-    import os
-    import subprocess
-    import sys
-    from tests.conftest import ROOT
-    code = ("import sys; sys.path.insert(0, %r)\n"
-            "from tests.oracle_lib import load_oracle\n"
-            "from tests.test_gpu_host_paths import test_strict_many_host_chunks\n"
-            "test_strict_many_host_chunks(load_oracle())\n"
-            "print('done', flush=True)\n" % ROOT)
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=ROOT,
-                       env=dict(os.environ, NWC_HOST_STREAM="0"))
-    assert r.returncode == 0 and "done" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-3000:])
-
-
-def test_strict_many_streamed_ragged(oracle):
-    """Streamed inputs at sizes that end inside a slice and inside a wave (16,384-equation slices,
-    64-equation waves), twice in a row on the same pinned buffer: verdicts equal the oracle's."""
+def test_strict_many_host_ragged(oracle):
+    """The chunked host pipeline at sizes that end inside a 64-equation wave and off every chunk
+    boundary, twice in a row on the same stages and arena: verdicts equal the oracle's."""
     from narwhal_amd import _lib
     lib = _lib.load()
     rng = np.random.default_rng(83)
