@@ -345,9 +345,11 @@ def test_launch_key_combs_grow_as_keys_join():
         return h.value, _lib.memory_info()["auto_cache"]
 
     comb = 155648 * 128   # KeyComb: 19 windows x 8,192 entries of 128 B
+    m0 = _lib.memory_info()["auto_cache"]   # the auto key cache alone (nwc_trim freed the launch keys)
     h1, m1 = launch(40, tag=1)
     h2, m2 = launch(100, tag=2)
     h3, m3 = launch(100, tag=3)
     assert (h1, h2, h3) == (40, 40, 100), (h1, h2, h3)
     assert m2 == m1 and m3 - m1 >= 60 * comb and m3 < m1 + 70 * comb, (m1, m2, m3)
-    assert m1 < 48 * comb + (400 << 20), m1
+    # (the first launch also builds the tables and the auto cache's first arrays if nothing had yet)
+    assert 40 * comb <= m1 - m0 < 40 * comb + (400 << 20) or (m0 == 0 and m1 < 40 * comb + (400 << 20)), (m0, m1)
