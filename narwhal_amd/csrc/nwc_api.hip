@@ -144,6 +144,8 @@ struct DevCtx {
   size_t scratch_cap = 0;
   uint32_t* fb_list = nullptr;     // lanes whose half-size reduction failed (k_verify_fallback)
   uint32_t* fb_count = nullptr;
+  uint8_t* pair_buf = nullptr;      // the paired strict host pipeline: per-chunk fallback counts + lists
+  size_t pair_cap = 0;
   uint64_t* stamps = nullptr;      // k_verify<.., STAMP>: 4 words per wave of the resident grid (nwc_diag_verify_clock)
   size_t fb_cap = 0;
   hipEvent_t scratch_free = nullptr;
@@ -800,7 +802,8 @@ int ensure_stager(DevCtx& d) {
 int release_idle_buffers(DevCtx& d, const uint8_t* in_use) {
   const size_t keep = verify_keep_bytes();
   struct Buf { uint8_t** p; size_t* cap; } bufs[] = {
-      {&d.straus_scratch, &d.straus_cap}, {&d.msm_scratch, &d.msm_cap}, {&d.rs_buf, &d.rs_cap}};
+      {&d.straus_scratch, &d.straus_cap}, {&d.msm_scratch, &d.msm_cap}, {&d.rs_buf, &d.rs_cap},
+      {&d.pair_buf, &d.pair_cap}};
   bool any = false;
   for (const Buf& b : bufs) any = any || (*b.p && *b.p != in_use && *b.cap > keep);
   if (!any) return 0;
@@ -826,6 +829,18 @@ int release_idle_buffers(DevCtx& d, const uint8_t* in_use) {
 // chunked sanitize pipeline: one set of those small launches per call instead of per chunk.
 constexpr int LV_ALL_CACHED = 1, LV_OUT_ZEROED = 2, LV_AUTO = 4, LV_STAMP = 8, LV_DEFER_LIST = 16;
 
+// One launch of the paired strict host pipeline (verify_range): launches on two streams may run at
+// the same time, so each takes half of the table slots (`half`; grid capped at half the persistent
+// grid) and lists its failed reductions in its own region of the fallback list with its own count;
+// the caller orders the slots against other launches (scratch_free), sized the list beforehand and
+// runs the fallback passes once the pipeline has joined (a fallback launch queued behind a chunk
+// would wait for free slots while the other stream's chunk holds them, stalling its stream).
+struct PairLaunch {
+  int half;
+  uint32_t* fb_list;
+  uint32_t* fb_count;
+};
+
 // launch_verify's comb path over the committee cache for any n (what LV_DEFER_LIST needs)
 bool deferrable_list(const DevCtx& d) {
   return verify_path() == VPath::Default && d.cm_n && d.cm_comb && d.comb16;
@@ -842,7 +857,8 @@ uint32_t force_fallback_every() {
 
 int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
-                  hipStream_t s, int flags = 0, uint8_t* vbytes = nullptr, uint64_t list_base = 0) {
+                  hipStream_t s, int flags = 0, uint8_t* vbytes = nullptr, uint64_t list_base = 0,
+                  const PairLaunch* pl = nullptr) {
   if (n == 0) return 0;
   if (int rc = ensure_verify_tables(d)) return rc;
   if (int rc = release_idle_buffers(d, nullptr)) return rc;
@@ -914,7 +930,9 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   // persistent grid: a few blocks per resident slot so the tail is short
   const uint64_t cap = (uint64_t)d.cus * d.verify_blocks_per_cu * NWC_VERIFY_GRID_MULT;
   size_t need = (size_t)cap * 256 * 2 * nwc::TAB_BYTES_PER_LANE;
-  const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
+  const bool pair = pl != nullptr;
+  const uint64_t gcap = pair ? cap / 2 : cap;
+  const unsigned grid = (unsigned)(tiles < gcap ? tiles : gcap);
   // comb grid: at most the resident blocks; tile t goes to block t mod grid, so every lane gets
   // ceil or floor of n / lanes equations (in chunks of COMB_BATCH sharing one inversion), and
   // a small n spreads one equation per lane
@@ -928,7 +946,9 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   if (int rc = ensure_scratch(d, need, defer ? d.fb_cap : n)) return rc;
   if (lk)
     if (int rc = lk_ensure(d, s)) return rc;
-  HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
+  if (pair && (!strict || comb || path == VPath::Full || d.cm_n))
+    return set_err(NWC_ERR_ARG, "paired launch off the strict half-size path");
+  if (!pair) HIP_TRY(hipStreamWaitEvent(s, d.scratch_free, 0));
   if (lk) {
     // the set's update is ordered after every launch that read it (scratch_free) and before this
     // launch's comb kernel; the builds exit at once when no key joined
@@ -944,6 +964,11 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
                                : nwc::Committee{d.cm_keys, d.cm_flags, d.cm_tables, d.cm_comb, d.cm_slots, d.cm_slot_mask, d.cm_n};
   nwc::VerifyArgs a{msgs, msg_index, msg_stride, pks, sigs, out_words, n, strict, d.base_table, d.base24, d.scratch,
                     d.fb_list, d.fb_count, force_every, cm};
+  if (pair) {
+    a.scratch = d.scratch + (size_t)(pl->half ? cap / 2 : 0) * 256 * 2 * nwc::TAB_BYTES_PER_LANE;
+    a.fb_list = pl->fb_list;
+    a.fb_count = pl->fb_count;
+  }
   a.force_windows = knobs().force_windows.load();
   a.stamps = d.stamps;
   const nwc::CombArgs ca{d.uc_list, d.uc_count, d.comb_base, d.comb16, nullptr, (uint32_t)(defer ? list_base : 0)};
@@ -952,7 +977,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   // lane per new key) runs on the side stream beside the verification instead of after it
   // a small batch no cache covers (first-sight keys): one limb-sliced block per equation, the
   // batch leaf's torsion test inside it
-  const bool cold = half && !comb && !cm.n && n <= cold_max() && cold_path();
+  const bool cold = half && !comb && !cm.n && n <= cold_max() && cold_path() && !pair;
   const bool tors_beside = !strict && !comb && n <= NWC_WIDE_MAX && !cold;
   if (tors_beside) {
     HIP_TRY(hipEventRecord(d.ev_fork, s));
@@ -971,7 +996,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     HIP_TRY(hipEventRecord(d.scratch_free, s));
     return 0;
   }
-  if (half) HIP_TRY(hipMemsetAsync(d.fb_count, 0, sizeof(uint32_t), s));
+  if (half) HIP_TRY(hipMemsetAsync(a.fb_count, 0, sizeof(uint32_t), s));
   if (comb) {
     HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
     if (n <= NWC_WIDE_MAX) {
@@ -1001,7 +1026,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
       hipLaunchKernelGGL((nwc::k_verify<false, false>), dim3(grid), dim3(256), 0, s, a, ca);
   }
   HIP_TRY(hipGetLastError());
-  if (half) {
+  if (half && !pair) {
     // lanes whose reduction failed are rare (|c| or d >= 2^147); a few blocks suffice
     const unsigned fgrid = grid < 16u ? grid : 16u;
     hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(fgrid), dim3(256), 0, s, a);
@@ -1016,7 +1041,7 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     if (int rc = launch_torsion(d, pks, out_words, n, comb ? d.uc_list : nullptr, comb ? d.uc_count : nullptr, cm, s))
       return rc;
   }
-  HIP_TRY(hipEventRecord(d.scratch_free, s));
+  if (!pair) HIP_TRY(hipEventRecord(d.scratch_free, s));
   return 0;
 }
 
@@ -1275,6 +1300,117 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     std::memcpy(out_words.data(), h, 8 * words);
     if (!(fl & LV_ALL_CACHED) && n <= NWC_WIDE_MAX && verify_path() == VPath::Default)
       if (int rc = auto_insert(d, pks + 32 * lo, n)) return rc;
+    return 0;
+  }
+  // Strict calls without a committee cache: the paired pipeline.  Chunks alternate between the
+  // device stream and the side stream, each launch on its own half of the table slots with its own
+  // fallback count and list region (PairLaunch), so chunk k + 1's blocks take the slots chunk k's
+  // drain frees instead of waiting for its last block, and the first chunk can be small
+  // (NWC_HOST_PAIR_FIRST, 65,536 equations = 8 MB of inputs, then x NWC_HOST_PAIR_GROWTH = 2).
+  // The fallback passes run once the streams have joined.  NWC_HOST_PAIR=0: the single-stream
+  // chunks below (A/B).
+  static const bool pair_on = [] {
+    const char* e = std::getenv("NWC_HOST_PAIR");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  static const uint64_t pair_first = [] {
+    const char* e = std::getenv("NWC_HOST_PAIR_FIRST");
+    return std::max<uint64_t>(64, (e ? std::strtoull(e, nullptr, 10) : 65536ull) / 64 * 64);
+  }();
+  static const uint64_t pair_growth = [] {
+    const char* e = std::getenv("NWC_HOST_PAIR_GROWTH");
+    return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 2ull;
+  }();
+  static const uint64_t pair_max = [] {
+    const char* e = std::getenv("NWC_HOST_PAIR_MAX");
+    return std::max<uint64_t>(64, (e ? std::strtoull(e, nullptr, 10) : 1ull << 20) / 64 * 64);
+  }();
+  if (pair_on && strict && !batch && verify_path() == VPath::Default && !d.cm_n && n >= 2 * pair_first &&
+      n <= verify_max_launch()) {
+    if (int rc = ensure_stager(d)) return rc;
+    if (int rc = ensure_verify_tables(d)) return rc;
+    if (int rc = release_idle_buffers(d, d.pair_buf)) return rc;
+    HostStager* const hs = d.stager.get();
+    hs->reset();
+    const auto tv0 = std::chrono::steady_clock::now();
+    std::vector<uint64_t> cuts{0};
+    uint64_t maxlen = 0;
+    for (uint64_t len = pair_first; cuts.back() < n; len = std::min(len * pair_growth, std::max(pair_first, pair_max))) {
+      uint64_t next = std::min<uint64_t>(n, cuts.back() + len);
+      if (n - next < pair_first / 2) next = n;   // no sliver of a last chunk
+      maxlen = std::max(maxlen, next - cuts.back());
+      cuts.push_back(next);
+    }
+    const uint64_t nch = cuts.size() - 1;
+    while (d.ev_chunk.size() < nch) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      d.ev_chunk.push_back(e);
+    }
+    // slots, lists and the per-chunk counts and list regions sized once, before any launch: inside
+    // the pipeline nothing is reallocated under a running chunk (hold_lists: no shrink either)
+    const uint64_t gcap = (uint64_t)d.cus * d.verify_blocks_per_cu * NWC_VERIFY_GRID_MULT;
+    if (int rc = ensure_scratch(d, (size_t)gcap * 256 * 2 * nwc::TAB_BYTES_PER_LANE, maxlen)) return rc;
+    const size_t counts_bytes = align256(4 * nch), pair_need = counts_bytes + 4 * n;
+    if (pair_need > d.pair_cap) {
+      HIP_TRY(hipEventSynchronize(d.scratch_free));
+      if (d.pair_buf) HIP_TRY(hipFree(d.pair_buf));
+      d.pair_buf = nullptr;
+      d.pair_cap = 0;
+      HIP_TRY(hipMalloc(&d.pair_buf, pair_need));
+      d.pair_cap = pair_need;
+    }
+    uint32_t* const counts = reinterpret_cast<uint32_t*>(d.pair_buf);
+    uint32_t* const lists = reinterpret_cast<uint32_t*>(d.pair_buf + counts_bytes);
+    struct Hold {
+      DevCtx& d;
+      ~Hold() { d.hold_lists = false; }
+    } hold{d};
+    d.hold_lists = true;
+    // the previous call's kernels may still read the arena and the slots: the copies wait for the
+    // device stream, both compute streams for scratch_free
+    HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
+    HIP_TRY(hipStreamWaitEvent(d.xfer, d.ev_fork, 0));
+    HIP_TRY(hipStreamWaitEvent(d.side, d.ev_fork, 0));
+    HIP_TRY(hipStreamWaitEvent(d.stream, d.scratch_free, 0));
+    HIP_TRY(hipStreamWaitEvent(d.side, d.scratch_free, 0));
+    auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+      return hs->put(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), bytes);
+    };
+    if (!msg_stride) HIP_TRY(h2d(dm, msgs, 32));
+    for (uint64_t k = 0; k < nch; ++k) {
+      const uint64_t c0 = cuts[k], len = cuts[k + 1] - cuts[k];
+      if (msg_stride) HIP_TRY(h2d(dm + 32 * c0, msgs + 32 * (lo + c0), 32 * len));
+      HIP_TRY(h2d(dp + 32 * c0, pks + 32 * (lo + c0), 32 * len));
+      HIP_TRY(h2d(ds + 64 * c0, sigs + 64 * (lo + c0), 64 * len));
+      HIP_TRY(hs->flush());
+      HIP_TRY(hipEventRecord(d.ev_chunk[k], d.xfer));
+      const hipStream_t sk = (k & 1) ? d.side : d.stream;
+      HIP_TRY(hipStreamWaitEvent(sk, d.ev_chunk[k], 0));
+      const PairLaunch pl{(int)(k & 1), lists + c0, counts + k};
+      if (int rc = launch_verify(d, msg_stride ? dm + 32 * c0 : dm, nullptr, msg_stride ? 1 : 0, dp + 32 * c0,
+                                 ds + 64 * c0, len, strict, dout + c0 / 64, sk, 0, nullptr, 0, &pl))
+        return rc;
+    }
+    HIP_TRY(hipEventRecord(d.ev_join, d.side));
+    HIP_TRY(hipStreamWaitEvent(d.stream, d.ev_join, 0));
+    // every chunk's failed reductions (rare: waves exit at once on an empty list)
+    for (uint64_t k = 0; k < nch; ++k) {
+      const uint64_t c0 = cuts[k], len = cuts[k + 1] - cuts[k];
+      const nwc::VerifyArgs a{msg_stride ? dm + 32 * c0 : dm, nullptr, msg_stride ? 1u : 0u, dp + 32 * c0, ds + 64 * c0,
+                              dout + c0 / 64, len, strict, d.base_table, d.base24, d.scratch, lists + c0, counts + k,
+                              0u, nwc::Committee{}};
+      hipLaunchKernelGGL(nwc::k_verify_fallback, dim3(16), dim3(256), 0, d.stream, a);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(d.scratch_free, d.stream));
+    const auto tq = std::chrono::steady_clock::now();
+    HIP_TRY(hipMemcpyAsync(out_words.data(), dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    if (host_timing())
+      std::fprintf(stderr, "nwc host call (paired): %llu equations in %llu chunks: copies queued after %.2f ms, done %.2f ms later\n",
+                   (unsigned long long)n, (unsigned long long)nch, std::chrono::duration<double>(tq - tv0).count() * 1e3,
+                   std::chrono::duration<double>(std::chrono::steady_clock::now() - tq).count() * 1e3);
     return 0;
   }
   static const uint64_t chunk = [] {
@@ -1778,6 +1914,7 @@ void nwc_shutdown(void) {
     if (d->scratch) (void)hipFree(d->scratch);
     if (d->fb_list) (void)hipFree(d->fb_list);
     if (d->fb_count) (void)hipFree(d->fb_count);
+    if (d->pair_buf) (void)hipFree(d->pair_buf);
     if (d->stamps) (void)hipFree(d->stamps);
     if (d->cm_keys) (void)hipFree(d->cm_keys);
     if (d->cm_flags) (void)hipFree(d->cm_flags);
@@ -2771,7 +2908,7 @@ int nwc_memory_info(nwc_memory* out) {
                                         (size_t)d.lk.cap * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad) +
                                         4 * (size_t)nwc::LK_SLOTS + 16
                                   : 0);
-    out->scratch = d.scratch_cap + d.straus_cap + d.msm_cap + d.rs_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap +
+    out->scratch = d.scratch_cap + d.straus_cap + d.msm_cap + d.rs_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap + d.pair_cap +
                    8 * (size_t)d.ts_slot_count;
   }
   out->digesters = digester_device_bytes(d.hip_id);

@@ -127,7 +127,7 @@ def main():
                  "straus_mismatch": 0, "randomized": 0, "straus_randomized_pass": 0} for c in CLASSES}
     host_batch = {"votes": 0, "certificates": 0, "bad_votes": 0, "failing_certificates": 0, "mismatch": 0}
     dalek = {"votes": 0, "certificates": 0, "failing_certificates": 0, "certificates_with_randomized_votes": 0,
-             "randomized_certificates_passed": 0, "mismatch": 0}
+             "randomized_certificates_passed": 0, "cert_mismatch": 0, "bad_vote_mismatch": 0, "mismatch": 0}
     t0 = time.time()
     done = 0
     mism = []
@@ -220,7 +220,12 @@ def main():
                                         zs[v0:v1], z8=True)
             with ThreadPoolExecutor(threads) as ex:
                 ocert = np.concatenate(list(ex.map(z8, parts)))
-            obad = ~ol.astype(bool) & ~np.repeat(ocert, counts)
+            # the votes' leaves against their certificate's digest (the mutations changed m, which
+            # the certificate path never reads): the bad set of a rejected certificate
+            olc = orc.leaf_many(np.ascontiguousarray(cdig[vote_cert]), p, s, threads=threads).astype(bool)
+            obad = ~olc & ~np.repeat(ocert, counts)
+            dalek["cert_mismatch"] += int((gcert != ocert).sum())
+            dalek["bad_vote_mismatch"] += int((gbad != obad).sum())
             dmis = int((gcert != ocert).sum()) + int((gbad != obad).sum())
             cls = orc.vote_class_many(m, p, s, threads=threads)
             csum = np.concatenate([[0], np.cumsum(cls == 1)])

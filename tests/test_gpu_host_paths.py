@@ -35,8 +35,9 @@ def test_strict_many_host_chunks(oracle):
 
 
 def test_strict_many_host_ragged(oracle):
-    """The chunked host pipeline at sizes that end inside a 64-equation wave and off every chunk
-    boundary, twice in a row on the same stages and arena: verdicts equal the oracle's."""
+    """The paired host pipeline (strict calls, no committee cache) at sizes that end inside a
+    64-equation wave and off every chunk boundary, twice in a row on the same stages and arena:
+    verdicts equal the oracle's."""
     from narwhal_amd import _lib
     lib = _lib.load()
     rng = np.random.default_rng(83)
@@ -53,6 +54,41 @@ def test_strict_many_host_ragged(oracle):
         exp = oracle.strict_many(msgs, pks, sigs)
         assert (got == exp).all(), (n, np.nonzero(got != exp)[0][:10])
         assert (exp == ~bad).all()
+
+
+@pytest.mark.parametrize("env", [{"NWC_HOST_PAIR_FIRST": "4096", "NWC_HOST_PAIR_GROWTH": "2"},
+                                 {"NWC_HOST_PAIR_FIRST": "8192", "NWC_HOST_PAIR_GROWTH": "1",
+                                  "NWC_FORCE_FALLBACK_EVERY": "3"},
+                                 {"NWC_HOST_PAIR": "0"}])
+def test_strict_many_host_pipelines(env, oracle, tmp_path):
+    """Strict host calls through the paired pipeline cut into many alternating chunks (each chunk
+    on its own half of the table slots and its own fallback list; one case sends every third
+    equation of each chunk through the fallback kernel) and through the single-stream chunks:
+    verdicts equal the oracle's, on two calls in a row.  Each case in its own process (libnwc
+    reads the switches once)."""
+    import os
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    rng = np.random.default_rng(84)
+    n = 150_001
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pks, sigs = oracle.keygen_sign_many(seeds, msgs)
+    bad = rng.random(n) < 0.01
+    bad[[4095, 4096, 8191, 8192, 12287, 12288, n - 1]] = True
+    sigs[bad, 9] ^= 2
+    exp = oracle.strict_many(msgs, pks, sigs)
+    assert (exp == ~bad).all()
+    inp, out = str(tmp_path / "in.npz"), str(tmp_path / "out.npz")
+    np.savez(inp, m=msgs, p=pks, s=sigs)
+    e = dict(os.environ)
+    e.update(env)
+    subprocess.run([sys.executable, os.path.join(ROOT, "tests", "host_pair_helper.py"), inp, out, ROOT], env=e,
+                   check=True, timeout=300)
+    r = np.load(out)
+    for k in ("first", "second"):
+        assert (r[k] == exp).all(), (env, k, np.nonzero(r[k] != exp)[0][:10])
 
 
 def test_batch_many_host_chunks(oracle):
