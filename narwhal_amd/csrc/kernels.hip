@@ -1530,6 +1530,153 @@ __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs c
   }
 }
 
+// ------------------------------------------------------------------------------- comb verify, sign deferred
+// k_verify_comb amortises each lane's inversion (~31k VALU instructions, 254 squarings) over the
+// lane's equations of the launch.  A launch of about one resident round (the message pipeline's
+// per-chunk leaf launches: ~160k votes on 131k lanes) gives a lane one or two equations, and the
+// inversion then costs as much as the rest of the equation: such launches ran at ~370 M votes/s
+// against ~640 M in a long launch.  Split the decision instead:
+//   k_verify_comb_y: R' = sB + k(-A) by the combs (as k_verify_comb), and y(R') == y_R tested
+//     projectively, Y == y_R Z (mod p): no inversion.  The vote's X and Z (canonical words) and a
+//     pending bit (key cached, flags, s < l, not small-order, Y test) go to SignRecs at the vote's
+//     call-wide index (list_base + i).  No verdict word is written.
+//   k_comb_sign: later, once over many votes, the sign of x(R') = X/Z against R's sign bit, with
+//     one inversion per lane over ~8 votes (Montgomery's trick along the lane's strided votes);
+//     writes the verdict words of its range (pending && sign ok; uncached keys are 0 here and are
+//     OR-ed in by the list pass that follows).
+// Same decision as k_verify_comb: y(R') == y_R mod p and sign(x(R')) == bit 255 of R (any sign
+// when x(R') = 0).
+struct SignRecs {
+  u32* x;      // 8 words per vote: X of R' (canonical)
+  u32* z;      // 8 words per vote: Z of R' (canonical; 1 when Z == 0)
+  u32* p;      // 8 words per vote: k_comb_sign's running product before the vote
+  u32* meta;   // bit 0 pending, bit 1 R's sign bit
+};
+
+// (bodies over blocks [blk, nblk) of the grid: k_verify_comb_y_sign runs both in one launch)
+__device__ __forceinline__ void comb_y_body(const VerifyArgs& a, const CombArgs& ca, const SignRecs& sr, uint32_t blk,
+                                            uint32_t nblk) {
+  const Committee& cm = a.committee;
+  const uint64_t stride = (uint64_t)nblk * blockDim.x;
+  for (uint64_t b0 = (uint64_t)blk * blockDim.x; b0 < a.n; b0 += stride) {   // block-uniform
+    const uint64_t i = b0 + threadIdx.x;
+    const bool active = i < a.n;
+    u32 mw[8], aw[8], sgw[16];
+    load_inputs(a, active ? i : 0, mw, aw, sgw);
+    const int key = committee_lookup(cm, aw);
+    if (active && key < 0) ca.list[atomicAdd(ca.count, 1u)] = ca.list_base + (uint32_t)i;
+    const int kk = key < 0 ? 0 : key;
+    u32 rw[8], sw[8];
+    _Pragma("unroll") for (int q = 0; q < 8; ++q) { rw[q] = sgw[q]; sw[q] = sgw[8 + q]; }
+    const fe yr = fe_from_words(rw);   // y_R mod p (bit 255 ignored)
+    u32 yw[8];
+    fe_to_words(yr, yw);
+    const u32 fl = cm.flags[kk];
+    const bool small = a.strict && ycanon_is_small_order(yw);
+    const bool ok = active && key >= 0 && sc_lt_l(sw) && key_flags_ok(fl, a.strict != 0) && !small;
+    ge_p2 q;
+    if (__any(key >= 0)) {
+      u32 kw[8];
+      challenge(rw, aw, mw, kw);
+      q = comb_sum(sw, kw, ca.comb16, cm.comb + (size_t)kk * COMB_PER_KEY);
+    } else {
+      q.X = fe_zero();
+      q.Y = fe_one();
+      q.Z = fe_one();
+    }
+    const bool zbad = fe_is_zero(q.Z);   // an undecodable key's off-curve comb (see k_verify_comb)
+    const bool ymatch = fe_is_zero(fe_sub(fe_mul(yr, q.Z), q.Y));
+    u32 xw[8], zw[8];
+    fe_to_words(q.X, xw);
+    fe_to_words(fe_select(q.Z, fe_one(), zbad), zw);
+    if (active) {
+      const uint64_t v = (uint64_t)ca.list_base + i;
+      uint4* xd = reinterpret_cast<uint4*>(sr.x + 8 * v);
+      uint4* zd = reinterpret_cast<uint4*>(sr.z + 8 * v);
+      xd[0] = make_uint4(xw[0], xw[1], xw[2], xw[3]);
+      xd[1] = make_uint4(xw[4], xw[5], xw[6], xw[7]);
+      zd[0] = make_uint4(zw[0], zw[1], zw[2], zw[3]);
+      zd[1] = make_uint4(zw[4], zw[5], zw[6], zw[7]);
+      sr.meta[v] = (ok && !zbad && ymatch ? 1u : 0u) | ((rw[7] >> 31) << 1);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void k_verify_comb_y(VerifyArgs a, CombArgs ca, SignRecs sr) {
+  comb_y_body(a, ca, sr, blockIdx.x, gridDim.x);
+}
+
+__device__ __forceinline__ fe load_fe_words(const u32* p) {
+  const uint4* s = reinterpret_cast<const uint4*>(p);
+  const uint4 u0 = s[0], u1 = s[1];
+  const u32 w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+  return fe_from_words(w);
+}
+
+// Votes [v0, v0 + n) of SignRecs (v0 a multiple of 64; the lane count a multiple of 64): lane l
+// takes votes v0 + l + j * lanes, so a wave's step j is one aligned verdict word.
+__device__ __forceinline__ void comb_sign_body(const SignRecs& sr, uint64_t v0, uint64_t n, uint64_t* out_bits,
+                                               uint32_t blk, uint32_t nblk) {
+  const uint64_t lanes = (uint64_t)nblk * blockDim.x;
+  const uint64_t l = (uint64_t)blk * blockDim.x + threadIdx.x;
+  const uint64_t wb = l & ~63ull;
+  const uint64_t steps = wb < n ? (n - wb + lanes - 1) / lanes : 0;   // wave-uniform
+  fe P = fe_one();
+#pragma unroll 1
+  for (uint64_t j = 0; j < steps; ++j) {
+    const uint64_t idx = l + j * lanes;
+    const bool active = idx < n;
+    const uint64_t v = v0 + (active ? idx : 0);
+    if (active) {
+      u32 pw[8];
+      fe_to_words(P, pw);
+      uint4* pd = reinterpret_cast<uint4*>(sr.p + 8 * v);
+      pd[0] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+      pd[1] = make_uint4(pw[4], pw[5], pw[6], pw[7]);
+    }
+    const fe z = active ? load_fe_words(sr.z + 8 * v) : fe_one();
+    P = fe_mul(P, z);
+  }
+  fe inv = fe_invert(P);
+#pragma unroll 1
+  for (uint64_t jj = steps; jj-- > 0;) {
+    const uint64_t idx = l + jj * lanes;
+    const bool active = idx < n;
+    const uint64_t v = v0 + (active ? idx : 0);
+    const fe pb = active ? load_fe_words(sr.p + 8 * v) : fe_one();
+    const fe z = active ? load_fe_words(sr.z + 8 * v) : fe_one();
+    const fe zi = fe_mul(inv, pb);
+    inv = fe_mul(inv, z);
+    u32 xw[8];
+    fe_to_words(fe_mul(load_fe_words(sr.x + 8 * v), zi), xw);
+    u32 xor_ = 0;
+    _Pragma("unroll") for (int q = 0; q < 8; ++q) xor_ |= xw[q];
+    const u32 m = sr.meta[v];
+    const bool sign_ok = xor_ == 0 || (xw[0] & 1) == ((m >> 1) & 1);
+    const uint64_t ballot = __ballot(active && (m & 1) && sign_ok);
+    if ((threadIdx.x & 63) == 0) out_bits[(v0 + wb + jj * lanes) >> 6] = ballot;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_comb_sign(SignRecs sr, uint64_t v0, uint64_t n, uint64_t* out_bits) {
+  comb_sign_body(sr, v0, n, out_bits, blockIdx.x, gridDim.x);
+}
+
+// One launch of both: blocks [0, sign_blocks) run the previous launch's sign tests (latency-bound:
+// one inversion per lane), the rest this launch's comb sums, so the sign pass's chain hides behind
+// the sums instead of standing alone on the leaf stream.
+struct SignPass {
+  uint64_t v0, n;
+  uint64_t* out_bits;
+  uint32_t blocks;
+};
+__global__ __launch_bounds__(256, 2) void k_verify_comb_y_sign(VerifyArgs a, CombArgs ca, SignRecs sr, SignPass sp) {
+  if (blockIdx.x < sp.blocks)
+    comb_sign_body(sr, sp.v0, sp.n, sp.out_bits, blockIdx.x, sp.blocks);
+  else
+    comb_y_body(a, ca, sr, blockIdx.x - sp.blocks, gridDim.x - sp.blocks);
+}
+
 // ------------------------------------------------------------------------------- committee latency
 // Latency form of the comb path for small batches (a certificate's votes, BASELINE cfg 1): one
 // equation per 128-thread block.  Wave 0 sums the 64 comb entries of sB + k(-A) with one entry per

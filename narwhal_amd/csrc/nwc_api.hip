@@ -858,7 +858,8 @@ uint32_t force_fallback_every() {
 int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uint64_t msg_stride,
                   const uint8_t* pks, const uint8_t* sigs, uint64_t n, int strict, uint64_t* out_words,
                   hipStream_t s, int flags = 0, uint8_t* vbytes = nullptr, uint64_t list_base = 0,
-                  const PairLaunch* pl = nullptr) {
+                  const PairLaunch* pl = nullptr, const nwc::SignRecs* sr = nullptr,
+                  const nwc::SignPass* sp = nullptr) {
   if (n == 0) return 0;
   if (int rc = ensure_verify_tables(d)) return rc;
   if (int rc = release_idle_buffers(d, nullptr)) return rc;
@@ -911,6 +912,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const bool defer = (flags & LV_DEFER_LIST) != 0;
   if (defer && (lk || !comb || list_base + n > d.fb_cap || !deferrable_list(d)))
     return set_err(NWC_ERR_ARG, "deferred list launch off the committee-cache comb path");
+  if (sr && (!defer || (list_base & 63)))
+    return set_err(NWC_ERR_ARG, "sign-deferred launch outside a word-aligned deferred list launch");
   if (comb && n <= NWC_WIDE_MAX && (flags & LV_ALL_CACHED)) {
     // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none).
     // The host checked every key against its view of the cache (set under g_cm_mu, like the
@@ -984,6 +987,18 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
     HIP_TRY(hipStreamWaitEvent(d.side, d.ev_fork, 0));
     if (int rc = launch_torsion(d, pks, out_words, n, nullptr, nullptr, cm, d.side, 1, 1)) return rc;
     HIP_TRY(hipEventRecord(d.ev_join, d.side));
+  }
+  if (defer && sr) {
+    // R' and the projective y test now, the sign of x(R') later in k_comb_sign over many votes
+    // (or in the first blocks of the next such launch: sp, the previous launch's votes)
+    const unsigned gy = (unsigned)std::min<uint64_t>(tiles, 60000);
+    if (sp && sp->n)
+      hipLaunchKernelGGL(nwc::k_verify_comb_y_sign, dim3(gy + sp->blocks), dim3(256), 0, s, a, ca, *sr, *sp);
+    else
+      hipLaunchKernelGGL(nwc::k_verify_comb_y, dim3(gy), dim3(256), 0, s, a, ca, *sr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(d.scratch_free, s));
+    return 0;
   }
   if (defer) {
     if (n <= NWC_WIDE_MAX) {
@@ -2481,6 +2496,22 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
   return 0;
 }
 
+// k_comb_sign over votes [v0, v0 + n) of sr (v0 a multiple of 64): about 8 votes per lane, so the
+// lane's one inversion is shared, and at most the resident comb lanes
+uint32_t comb_sign_blocks(const DevCtx& d, uint64_t n) {
+  constexpr uint64_t per = 8;   // votes per lane
+  const uint64_t resident = (uint64_t)d.cus * d.comb_blocks_per_cu;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, (n + 256 * per - 1) / (256 * per)));
+}
+int launch_comb_sign(DevCtx& d, const nwc::SignRecs& sr, uint64_t v0, uint64_t n, uint64_t* out_bits, hipStream_t s) {
+  if (n == 0) return 0;
+  if (v0 & 63) return set_err(NWC_ERR_ARG, "sign pass off a verdict word");
+  const uint32_t blocks = comb_sign_blocks(d, n);
+  hipLaunchKernelGGL(nwc::k_comb_sign, dim3(blocks), dim3(256), 0, s, sr, v0, n, out_bits);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 // Device part of nwc_sanitize_messages: messages in HBM (ddata 4-byte aligned with >= 16 bytes
 // of readable padding, doff device u64[m+1] relative to ddata, `total` bytes), parsed as the
 // chunks cuts[k] .. cuts[k+1] (whole messages).  `chunk_ready(k)`, when given, returns once chunk
@@ -2504,9 +2535,23 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   // a vote list is allocated only when wholly inside its message (>= 72 B per vote)
   const uint64_t vt = total / 72 + 1 + (nch > 1 ? 64 * nch : 0);   // + the 64-slot alignment of each chunk
   if (vt > 0xFFFFFFFFull) return set_err(NWC_ERR_ARG, "too many vote slots in one call");
+  // the leaf launches of a chunked call on the committee-cache comb path only list their uncached
+  // equations (LV_DEFER_LIST); the list's half-size, fallback and torsion passes run once, after
+  // the leaves queued before the first strict launch (which reuses the list), instead of ~8 small
+  // launches per chunk on the leaf stream.  Their sign tests are deferred too (SignRecs,
+  // k_verify_comb_y / k_comb_sign): a chunk's ~1 vote per lane would otherwise pay a whole
+  // inversion per vote.  NWC_SIGN_DEFER=0: k_verify_comb per chunk (A/B).
+  const bool chunked = nch > 1;
+  const bool defer = chunked && deferrable_list(d);
+  static const bool sign_defer_on = [] {
+    const char* e = std::getenv("NWC_SIGN_DEFER");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  const bool ysplit = defer && sign_defer_on;
   const size_t need = align256(total + 128 * (m + 2)) + align256(32 * m) * 3 + align256(64 * m) + align256(32 * vt) +
                       align256(64 * vt) + align256(4 * vt) + align256(4) + align256(4 * m) + align256(16 * m) +
-                      align256(4 * m) + align256(8 * ((m + 63) / 64)) + align256(8 * ((vt + 63) / 64));
+                      align256(4 * m) + align256(8 * ((m + 63) / 64)) + align256(8 * ((vt + 63) / 64)) +
+                      (ysplit ? 3 * align256(32 * vt) + align256(4 * vt) : 0);
   if (need > d.msg_arena_cap) {
     HIP_TRY(hipEventSynchronize(d.scratch_free));
     HIP_TRY(hipStreamSynchronize(s));
@@ -2538,6 +2583,13 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   a.rec_n = c.take<uint32_t>(4 * m);
   uint64_t* sbits = c.take<uint64_t>(8 * ((m + 63) / 64));
   uint64_t* lbits = c.take<uint64_t>(8 * ((vt + 63) / 64));
+  nwc::SignRecs sr{};
+  if (ysplit) {
+    sr.x = c.take<uint32_t>(32 * vt);
+    sr.z = c.take<uint32_t>(32 * vt);
+    sr.p = c.take<uint32_t>(32 * vt);
+    sr.meta = c.take<uint32_t>(4 * vt);
+  }
   a.digests = ddigests;
   if (vote_target) {
     a.target.enabled = 1;
@@ -2556,13 +2608,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   // the leaf stream when chunks overlap: the side stream, which has a hardware queue of its own
   // (GPU_MAX_HW_QUEUES = 4: a stream created later shared the transfer stream's queue, and its
   // leaves waited behind the markers of the in-flight copies, profiles/r05/wire_host.md)
-  const bool chunked = nch > 1;
   const hipStream_t ls = chunked ? d.side : s;
-  // the leaf launches of a chunked call on the committee-cache comb path only list their uncached
-  // equations (LV_DEFER_LIST); the list's half-size, fallback and torsion passes run once, after
-  // the leaves queued before the first strict launch (which reuses the list), instead of ~8 small
-  // launches per chunk on the leaf stream
-  const bool defer = chunked && deferrable_list(d);
   struct HoldLists {
     DevCtx& d;
     ~HoldLists() { d.hold_lists = false; }
@@ -2587,21 +2633,62 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     if (timing) marks.emplace_back(what, std::chrono::duration<double>(std::chrono::steady_clock::now() - tm0).count() * 1e3);
   };
   uint64_t launched = 0;   // votes [0, launched) have their leaf launch queued
+  bool list_dirty = false;   // a strict launch on ls has reused the uncached list since its reset
+  // ysplit: votes [owed_lo, owed_hi) have had their leaves but not their sign tests yet; those run
+  // in the first blocks of the next chunk's leaf launch (k_verify_comb_y_sign), so their
+  // latency-bound chain overlaps its comb sums, or alone before a list pass needs their words
+  uint64_t owed_lo = 0, owed_hi = 0;
   auto leaves = [&](uint64_t upto, bool deferred) -> int {
     if (upto <= launched) return 0;
-    const int rc = launch_verify(d, a.cdig, a.v_msg + launched, 0, a.v_pk + 32 * launched, a.v_sig + 64 * launched,
-                                 upto - launched, 0, lbits + launched / 64, ls, deferred ? LV_DEFER_LIST : 0, nullptr,
-                                 launched);
+    if (deferred && list_dirty) {
+      HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), ls));
+      list_dirty = false;
+    }
+    const uint64_t v0 = launched;
+    const bool y = deferred && ysplit;
+    const nwc::SignPass sp{owed_lo, owed_hi - owed_lo, lbits, comb_sign_blocks(d, owed_hi - owed_lo)};
+    if (int rc = launch_verify(d, a.cdig, a.v_msg + v0, 0, a.v_pk + 32 * v0, a.v_sig + 64 * v0, upto - v0, 0,
+                               lbits + v0 / 64, ls, deferred ? LV_DEFER_LIST : 0, nullptr, v0, nullptr,
+                               y ? &sr : nullptr, y ? &sp : nullptr))
+      return rc;
+    if (y) {
+      owed_lo = v0;
+      owed_hi = upto;
+    }
     pending = pending || deferred;
     launched = upto;
     mark("leaves queued");
-    return rc;
+    return 0;
   };
+  // the list passes of the deferred leaves so far (they OR the uncached votes' bits into the words
+  // the comb or sign kernels wrote), after the sign tests still owed
   auto finish = [&]() -> int {
+    if (owed_hi > owed_lo) {
+      if (int rc = launch_comb_sign(d, sr, owed_lo, owed_hi - owed_lo, lbits, ls)) return rc;
+      owed_lo = owed_hi;
+    }
     if (!pending) return 0;
     pending = false;
     return finish_deferred_list(d, a.cdig, a.v_msg, 0, a.v_pk, a.v_sig, launched, 0, lbits, ls);
   };
+  // the strict equations (headers' and votes' own signatures) of messages [c0, c1) on the leaf
+  // stream, after the list passes (the strict launch reuses the list)
+  auto strict = [&](size_t c0, size_t c1) -> int {
+    if (c1 <= c0) return 0;
+    if (int rc = finish()) return rc;
+    list_dirty = true;
+    return launch_verify(d, a.eq_msg + 32 * c0, nullptr, 1, a.eq_pk + 32 * c0, a.eq_sig + 64 * c0, c1 - c0, 1,
+                         sbits + c0 / 64, ls);
+  };
+  // The strict equations of the first chunks go in one launch after chunk strict_at's leaves,
+  // early, where the leaf stream has slack to absorb its ~0.17 ms (a latency-bound launch); the
+  // rest at the end (every cut is a multiple of 64 messages, sanitize_range: each strict launch
+  // owns its verdict words).  (A strict launch per chunk, each after a list pass, measured 20 %
+  // slower; at chunk nch - 3 instead of nch / 3, within noise: profiles/r06/wire_sign/.)
+  bool aligned = true;
+  for (size_t k = 1; k < nch; ++k) aligned = aligned && (cuts[k] & 63) == 0;
+  const size_t strict_at = aligned && nch >= 3 ? nch / 3 : (nch >= 2 ? nch - 2 : 0);   // its iteration k
+  size_t strict_done = 0;   // messages [0, strict_done) have their strict launch queued
   uint64_t nv = 0;
   size_t queued = 0;   // chunks whose parse is queued
   auto queue_parse = [&]() -> int {
@@ -2654,11 +2741,9 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     // (the last leaf launch then holds only the last chunk's votes)
     if (k + 1 < nch)
       if (int rc = leaves(nv, defer)) return rc;
-    // the strict equations of every chunk but the last while the last one crosses PCIe
-    // (cuts[nch - 1] is a multiple of 64 messages: the two strict launches own their words)
-    if (k + 2 == nch) {
-      if (int rc = finish()) return rc;
-      if (int rc = launch_verify(d, a.eq_msg, nullptr, 1, a.eq_pk, a.eq_sig, cuts[k + 1], 1, sbits, ls)) return rc;
+    if (k == strict_at) {
+      if (int rc = strict(0, cuts[k + 1])) return rc;
+      strict_done = cuts[k + 1];
     }
     if (queued == k + 1 && queued < nch)
       if (int rc = queue_parse()) return rc;
@@ -2668,11 +2753,15 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     // number of messages, so not per chunk)
     hipLaunchKernelGGL(nwc::k_header_digests, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, a);
     HIP_TRY(hipGetLastError());
-    const size_t c0 = cuts[nch - 1];
-    if (int rc = launch_verify(d, a.eq_msg + 32 * c0, nullptr, 1, a.eq_pk + 32 * c0, a.eq_sig + 64 * c0, m - c0, 1,
-                               sbits + c0 / 64, ls))
-      return rc;
-    if (int rc = leaves(nv, false)) return rc;
+    if (ysplit) {
+      // the last chunk's leaves deferred as well (a fresh list: the strict launch reused it),
+      // their sign tests, then the list passes and the remaining strict equations
+      if (int rc = leaves(nv, true)) return rc;
+      if (int rc = strict(strict_done, m)) return rc;
+    } else {
+      if (int rc = strict(strict_done, m)) return rc;
+      if (int rc = leaves(nv, false)) return rc;
+    }
     HIP_TRY(hipEventRecord(d.ev_msg, ls));
     HIP_TRY(hipStreamWaitEvent(s, d.ev_msg, 0));
   } else {
@@ -2758,8 +2847,10 @@ static int sanitize_range(int di, const uint8_t* data, const uint64_t* offsets, 
     uint64_t at = 0, next = std::min<uint64_t>(msg_chunk, 2 * lo);
     while (total - at > 2 * lo) {
       const uint64_t want = std::max(lo, std::min(next, (total - at) / 2));
-      const size_t cm = (size_t)(std::lower_bound(hoff.begin(), hoff.end(), at + want) - hoff.begin());
-      if (cm <= cuts.back() || cm >= m) break;
+      // every cut on a multiple of 64 messages: each chunk's strict launch owns its verdict words
+      size_t cm = (size_t)(std::lower_bound(hoff.begin(), hoff.end(), at + want) - hoff.begin()) & ~(size_t)63;
+      if (cm <= cuts.back()) cm = cuts.back() + 64;
+      if (cm >= m) break;
       cuts.push_back(cm);
       at = hoff[cm];
       next = std::min<uint64_t>(msg_chunk, 2 * next);
@@ -2935,6 +3026,8 @@ int nwc_trim(void) {
   d.msm_scratch = nullptr; d.msm_cap = 0;
   if (d.rs_buf) HIP_TRY(hipFree(d.rs_buf));
   d.rs_buf = nullptr; d.rs_cap = 0;
+  if (d.pair_buf) HIP_TRY(hipFree(d.pair_buf));
+  d.pair_buf = nullptr; d.pair_cap = 0;
   if (d.arena) HIP_TRY(hipFree(d.arena));
   if (d.msg_arena) HIP_TRY(hipFree(d.msg_arena));
   d.scratch = nullptr; d.scratch_cap = 0;

@@ -167,12 +167,14 @@ def test_sanitize_messages_host_staged():
     _sanitize_tiled_golden()
 
 
-def test_sanitize_messages_host_chunks():
+@pytest.mark.parametrize("sign_defer", ["1", "0"])
+def test_sanitize_messages_host_chunks(sign_defer):
     """The same batch in 1-MB pipelined chunks (NWC_MSG_CHUNK, read once per process: a child
-    process) -- the production pipeline forced to ~8 chunks cut on message boundaries, sharing one
-    64-aligned vote counter, each parsed while the previous one's leaves run on the side stream --
-    codes and digests unchanged.  (Round 6 removed the pipeline's A/B switches that lost or tied:
-    profiles/r05/wire_host.md.)"""
+    process) -- the production pipeline forced to ~8 chunks cut on 64-message boundaries, sharing
+    one 64-aligned vote counter, each parsed while the previous one's leaves run on the side stream,
+    with the leaves' sign tests deferred (k_verify_comb_y / k_verify_comb_y_sign / k_comb_sign) or
+    decided in k_verify_comb (NWC_SIGN_DEFER=0) -- codes and digests unchanged.  (Round 6 removed
+    the pipeline's A/B switches that lost or tied: profiles/r05/wire_host.md.)"""
     import os
     import subprocess
     import sys
@@ -182,7 +184,8 @@ def test_sanitize_messages_host_chunks():
             "_sanitize_tiled_golden()\n"
             "print('done', flush=True)\n" % ROOT)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=ROOT,
-                       env=dict(os.environ, NWC_MSG_CHUNK=str(1 << 20), NWC_HOST_TIMING="1"))
+                       env=dict(os.environ, NWC_MSG_CHUNK=str(1 << 20), NWC_HOST_TIMING="1",
+                                NWC_SIGN_DEFER=sign_defer))
     assert r.returncode == 0 and "done" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-3000:])
     steps = [l for l in r.stderr.splitlines() if l.startswith("nwc sanitize steps:")]
     assert steps and all(l.count("parse queued") >= 4 for l in steps), r.stderr[-2000:]   # several chunks
