@@ -1537,13 +1537,13 @@ __global__ __launch_bounds__(256, 2) void k_verify_comb(VerifyArgs a, CombArgs c
 // inversion then costs as much as the rest of the equation: such launches ran at ~370 M votes/s
 // against ~640 M in a long launch.  Split the decision instead:
 //   k_verify_comb_y: R' = sB + k(-A) by the combs (as k_verify_comb), and y(R') == y_R tested
-//     projectively, Y == y_R Z (mod p): no inversion.  The vote's X and Z (canonical words) and a
-//     pending bit (key cached, flags, s < l, not small-order, Y test) go to SignRecs at the vote's
-//     call-wide index (list_base + i).  No verdict word is written.
+//     projectively, Y == y_R Z (mod p): no inversion.  Equation i's X and Z (canonical words) and
+//     a pending bit (key cached, flags, s < l, not small-order, Y test) go to record i of SignRecs
+//     (the caller offsets the arrays).  No verdict word is written.
 //   k_comb_sign: later, once over many votes, the sign of x(R') = X/Z against R's sign bit, with
 //     one inversion per lane over ~8 votes (Montgomery's trick along the lane's strided votes);
-//     writes the verdict words of its range (pending && sign ok; uncached keys are 0 here and are
-//     OR-ed in by the list pass that follows).
+//     ORs pending && sign ok into the verdict words of its range, which the caller zeroed (the
+//     uncached keys' list passes OR theirs in too, before or after).
 // Same decision as k_verify_comb: y(R') == y_R mod p and sign(x(R')) == bit 255 of R (any sign
 // when x(R') = 0).
 struct SignRecs {
@@ -1590,7 +1590,7 @@ __device__ __forceinline__ void comb_y_body(const VerifyArgs& a, const CombArgs&
     fe_to_words(q.X, xw);
     fe_to_words(fe_select(q.Z, fe_one(), zbad), zw);
     if (active) {
-      const uint64_t v = (uint64_t)ca.list_base + i;
+      const uint64_t v = i;
       uint4* xd = reinterpret_cast<uint4*>(sr.x + 8 * v);
       uint4* zd = reinterpret_cast<uint4*>(sr.z + 8 * v);
       xd[0] = make_uint4(xw[0], xw[1], xw[2], xw[3]);
@@ -1613,8 +1613,9 @@ __device__ __forceinline__ fe load_fe_words(const u32* p) {
   return fe_from_words(w);
 }
 
-// Votes [v0, v0 + n) of SignRecs (v0 a multiple of 64; the lane count a multiple of 64): lane l
-// takes votes v0 + l + j * lanes, so a wave's step j is one aligned verdict word.
+// Votes [v0, v0 + n) (v0 a multiple of 64; the lane count a multiple of 64), vote v's record at
+// index v of sr (the caller offsets the arrays): lane l takes votes v0 + l + j * lanes, so a
+// wave's step j is one aligned verdict word.
 __device__ __forceinline__ void comb_sign_body(const SignRecs& sr, uint64_t v0, uint64_t n, uint64_t* out_bits,
                                                uint32_t blk, uint32_t nblk) {
   const uint64_t lanes = (uint64_t)nblk * blockDim.x;
@@ -1654,7 +1655,7 @@ __device__ __forceinline__ void comb_sign_body(const SignRecs& sr, uint64_t v0, 
     const u32 m = sr.meta[v];
     const bool sign_ok = xor_ == 0 || (xw[0] & 1) == ((m >> 1) & 1);
     const uint64_t ballot = __ballot(active && (m & 1) && sign_ok);
-    if ((threadIdx.x & 63) == 0) out_bits[(v0 + wb + jj * lanes) >> 6] = ballot;
+    if ((threadIdx.x & 63) == 0) out_bits[(v0 + wb + jj * lanes) >> 6] |= ballot;   // the word is this wave's
   }
 }
 
@@ -1666,13 +1667,14 @@ __global__ __launch_bounds__(256) void k_comb_sign(SignRecs sr, uint64_t v0, uin
 // one inversion per lane), the rest this launch's comb sums, so the sign pass's chain hides behind
 // the sums instead of standing alone on the leaf stream.
 struct SignPass {
+  SignRecs rec;   // the previous launch's records (vote v at index v)
   uint64_t v0, n;
   uint64_t* out_bits;
   uint32_t blocks;
 };
 __global__ __launch_bounds__(256, 2) void k_verify_comb_y_sign(VerifyArgs a, CombArgs ca, SignRecs sr, SignPass sp) {
   if (blockIdx.x < sp.blocks)
-    comb_sign_body(sr, sp.v0, sp.n, sp.out_bits, blockIdx.x, sp.blocks);
+    comb_sign_body(sp.rec, sp.v0, sp.n, sp.out_bits, blockIdx.x, sp.blocks);
   else
     comb_y_body(a, ca, sr, blockIdx.x - sp.blocks, gridDim.x - sp.blocks);
 }

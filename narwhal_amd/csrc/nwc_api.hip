@@ -146,6 +146,9 @@ struct DevCtx {
   uint32_t* fb_count = nullptr;
   uint8_t* pair_buf = nullptr;      // the paired strict host pipeline: per-chunk fallback counts + lists
   size_t pair_cap = 0;
+  uint8_t* sign_buf = nullptr;      // large host calls on the comb path: two chunks' SignRecs
+  size_t sign_cap = 0;
+  const uint8_t* busy_buf = nullptr;   // a buffer a host pipeline's launches use: never released under it
   uint64_t* stamps = nullptr;      // k_verify<.., STAMP>: 4 words per wave of the resident grid (nwc_diag_verify_clock)
   size_t fb_cap = 0;
   hipEvent_t scratch_free = nullptr;
@@ -803,13 +806,14 @@ int release_idle_buffers(DevCtx& d, const uint8_t* in_use) {
   const size_t keep = verify_keep_bytes();
   struct Buf { uint8_t** p; size_t* cap; } bufs[] = {
       {&d.straus_scratch, &d.straus_cap}, {&d.msm_scratch, &d.msm_cap}, {&d.rs_buf, &d.rs_cap},
-      {&d.pair_buf, &d.pair_cap}};
+      {&d.pair_buf, &d.pair_cap}, {&d.sign_buf, &d.sign_cap}};
+  auto idle = [&](const Buf& b) { return *b.p && *b.p != in_use && *b.p != d.busy_buf && *b.cap > keep; };
   bool any = false;
-  for (const Buf& b : bufs) any = any || (*b.p && *b.p != in_use && *b.cap > keep);
+  for (const Buf& b : bufs) any = any || idle(b);
   if (!any) return 0;
   HIP_TRY(hipEventSynchronize(d.scratch_free));
   for (const Buf& b : bufs) {
-    if (*b.p && *b.p != in_use && *b.cap > keep) {
+    if (idle(b)) {
       HIP_TRY(hipFree(*b.p));
       *b.p = nullptr;
       *b.cap = 0;
@@ -912,8 +916,8 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   const bool defer = (flags & LV_DEFER_LIST) != 0;
   if (defer && (lk || !comb || list_base + n > d.fb_cap || !deferrable_list(d)))
     return set_err(NWC_ERR_ARG, "deferred list launch off the committee-cache comb path");
-  if (sr && (!defer || (list_base & 63)))
-    return set_err(NWC_ERR_ARG, "sign-deferred launch outside a word-aligned deferred list launch");
+  if (sr && (!comb || (defer && (list_base & 63))))
+    return set_err(NWC_ERR_ARG, "sign-deferred launch off the comb path or off a verdict word");
   if (comb && n <= NWC_WIDE_MAX && (flags & LV_ALL_CACHED)) {
     // latency path, one launch: no scratch, no uncached list, no fallback (the comb path has none).
     // The host checked every key against its view of the cache (set under g_cm_mu, like the
@@ -1014,7 +1018,16 @@ int launch_verify(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_index, uin
   if (half) HIP_TRY(hipMemsetAsync(a.fb_count, 0, sizeof(uint32_t), s));
   if (comb) {
     HIP_TRY(hipMemsetAsync(d.uc_count, 0, sizeof(uint32_t), s));
-    if (n <= NWC_WIDE_MAX) {
+    if (sr) {
+      // sign test deferred (the chunked host path, verify_range): the words zeroed for the list
+      // passes and the later sign pass to OR into; the previous chunk's sign pass in front
+      HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
+      const unsigned gy = (unsigned)std::min<uint64_t>(tiles, 60000);
+      if (sp && sp->n)
+        hipLaunchKernelGGL(nwc::k_verify_comb_y_sign, dim3(gy + sp->blocks), dim3(256), 0, s, a, ca, *sr, *sp);
+      else
+        hipLaunchKernelGGL(nwc::k_verify_comb_y, dim3(gy), dim3(256), 0, s, a, ca, *sr);
+    } else if (n <= NWC_WIDE_MAX) {
       // small batches: one block per equation, critical path = one square root
       HIP_TRY(hipMemsetAsync(out_words, 0, 8 * ((n + 63) / 64), s));
       hipLaunchKernelGGL(nwc::k_verify_comb_wide, dim3((unsigned)n), dim3(128), 0, s, a, ca);
@@ -1092,6 +1105,41 @@ int finish_deferred_list(DevCtx& d, const uint8_t* msgs, const uint32_t* msg_ind
   return 0;
 }
 
+// sr with its arrays moved by `off` records (record i of the result is record i + off of sr)
+nwc::SignRecs sign_recs_at(const nwc::SignRecs& r, int64_t off) {
+  return nwc::SignRecs{r.x + 8 * off, r.z + 8 * off, r.p + 8 * off, r.meta + off};
+}
+// k_comb_sign over votes [v0, v0 + n) of sr (v0 a multiple of 64): about 8 votes per lane, so the
+// lane's one inversion is shared, and at most the resident comb lanes
+uint32_t comb_sign_blocks(const DevCtx& d, uint64_t n) {
+  constexpr uint64_t per = 8;   // votes per lane
+  const uint64_t resident = (uint64_t)d.cus * d.comb_blocks_per_cu;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, (n + 256 * per - 1) / (256 * per)));
+}
+int launch_comb_sign(DevCtx& d, const nwc::SignRecs& sr, uint64_t v0, uint64_t n, uint64_t* out_bits, hipStream_t s) {
+  if (n == 0) return 0;
+  if (v0 & 63) return set_err(NWC_ERR_ARG, "sign pass off a verdict word");
+  const uint32_t blocks = comb_sign_blocks(d, n);
+  hipLaunchKernelGGL(nwc::k_comb_sign, dim3(blocks), dim3(256), 0, s, sr, v0, n, out_bits);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// NWC_SIGN_DEFER=0: the comb path decides the sign in k_verify_comb everywhere (A/B of the
+// deferred sign tests of chunked launches: the message pipeline and large host calls)
+bool sign_defer() {
+  static const bool on = [] {
+    const char* e = std::getenv("NWC_SIGN_DEFER");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+// Whether launch_verify takes the comb path (k_verify_comb) for a plain launch of n equations.
+bool takes_comb_path(const DevCtx& d, uint64_t n, int strict) {
+  if (verify_path() != VPath::Default) return false;
+  const bool lk = !strict && !d.cm_n && d.comb16 && n >= nwc::LK_MIN_EQUATIONS && knobs().launch_keys.load();
+  return lk || (d.cm_n && d.cm_comb && (n <= NWC_WIDE_MAX || d.comb16));
+}
 // NWC_DIGEST_SCHED=0/1 forces the one-lane-per-message / scheduled digest kernel (A/B and tests).
 int digest_sched_mode() {
   static const int mode = [] {
@@ -1379,9 +1427,13 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
     uint32_t* const lists = reinterpret_cast<uint32_t*>(d.pair_buf + counts_bytes);
     struct Hold {
       DevCtx& d;
-      ~Hold() { d.hold_lists = false; }
+      ~Hold() {
+        d.hold_lists = false;
+        d.busy_buf = nullptr;
+      }
     } hold{d};
     d.hold_lists = true;
+    d.busy_buf = d.pair_buf;
     // the previous call's kernels may still read the arena and the slots: the copies wait for the
     // device stream, both compute streams for scratch_free
     HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
@@ -1469,6 +1521,41 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
       HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       d.ev_chunk.push_back(e);
     }
+    // Chunks on the comb path (launch keys or the committee cache) defer their sign tests: a
+    // lane gets ~8 votes of a 1M-vote chunk, and its one inversion would be ~9 % of each vote's
+    // work (k_verify_comb_y; the sign pass of chunk k runs in the first blocks of chunk k + 1's
+    // launch, the last one alone; SignRecs of two chunks alternate in sign_buf)
+    uint64_t maxlen = 0;
+    for (uint64_t k = 0; k < nch; ++k) maxlen = std::max(maxlen, cuts[k + 1] - cuts[k]);
+    const bool ysplit = !strict && sign_defer();
+    nwc::SignRecs reg[2] = {};
+    if (ysplit) {
+      if (int rc = release_idle_buffers(d, d.sign_buf)) return rc;
+      const size_t per = align256(32 * maxlen);
+      const size_t need_s = 2 * (3 * per + align256(4 * maxlen));
+      if (need_s > d.sign_cap) {
+        HIP_TRY(hipEventSynchronize(d.scratch_free));
+        if (d.sign_buf) HIP_TRY(hipFree(d.sign_buf));
+        d.sign_buf = nullptr;
+        d.sign_cap = 0;
+        HIP_TRY(hipMalloc(&d.sign_buf, need_s));
+        d.sign_cap = need_s;
+      }
+      Carve cs(d.sign_buf);
+      for (auto& r : reg) {
+        r.x = cs.take<uint32_t>(32 * maxlen);
+        r.z = cs.take<uint32_t>(32 * maxlen);
+        r.p = cs.take<uint32_t>(32 * maxlen);
+        r.meta = cs.take<uint32_t>(4 * maxlen);
+      }
+    }
+    uint64_t owed_c0 = 0, owed_len = 0;   // the chunk whose sign tests are still to run
+    int owed_reg = 0;
+    struct Busy {
+      DevCtx& d;
+      ~Busy() { d.busy_buf = nullptr; }
+    } busy{d};
+    d.busy_buf = d.sign_buf;
     // the previous call's kernels may still read the arena: the transfers wait for the stream
     HIP_TRY(hipEventRecord(d.ev_fork, d.stream));
     HIP_TRY(hipStreamWaitEvent(d.xfer, d.ev_fork, 0));
@@ -1491,10 +1578,27 @@ int verify_range(int di, const uint8_t* msgs, uint64_t msg_stride, const uint32_
       HIP_TRY(hs->flush());
       HIP_TRY(hipEventRecord(d.ev_chunk[k], d.xfer));
       HIP_TRY(hipStreamWaitEvent(d.stream, d.ev_chunk[k], 0));
+      const nwc::SignPass sp{sign_recs_at(reg[owed_reg], -(int64_t)owed_c0), owed_c0, owed_len, dout,
+                             comb_sign_blocks(d, owed_len)};
+      const bool y = ysplit && takes_comb_path(d, len, strict);
+      if (!y && owed_len) {
+        if (int rc = launch_comb_sign(d, sp.rec, owed_c0, owed_len, dout, d.stream)) return rc;
+        owed_len = 0;
+      }
+      const int r = (int)(k & 1);
       if (int rc = launch_verify(d, msg_stride ? dm + 32 * c0 : dm, batch ? dmi + c0 : nullptr, msg_stride ? 1 : 0,
-                                 dp + 32 * c0, ds + 64 * c0, len, strict, dout + c0 / 64, d.stream))
+                                 dp + 32 * c0, ds + 64 * c0, len, strict, dout + c0 / 64, d.stream, 0, nullptr, 0,
+                                 nullptr, y ? &reg[r] : nullptr, y && owed_len ? &sp : nullptr))
         return rc;
+      if (y) {
+        owed_c0 = c0;
+        owed_len = len;
+        owed_reg = r;
+      }
     }
+    if (owed_len)
+      if (int rc = launch_comb_sign(d, sign_recs_at(reg[owed_reg], -(int64_t)owed_c0), owed_c0, owed_len, dout, d.stream))
+        return rc;
     const auto tq = std::chrono::steady_clock::now();
     HIP_TRY(hipMemcpyAsync(out_words.data(), dout, 8 * words, hipMemcpyDeviceToHost, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
@@ -1930,6 +2034,7 @@ void nwc_shutdown(void) {
     if (d->fb_list) (void)hipFree(d->fb_list);
     if (d->fb_count) (void)hipFree(d->fb_count);
     if (d->pair_buf) (void)hipFree(d->pair_buf);
+    if (d->sign_buf) (void)hipFree(d->sign_buf);
     if (d->stamps) (void)hipFree(d->stamps);
     if (d->cm_keys) (void)hipFree(d->cm_keys);
     if (d->cm_flags) (void)hipFree(d->cm_flags);
@@ -2496,22 +2601,6 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
   return 0;
 }
 
-// k_comb_sign over votes [v0, v0 + n) of sr (v0 a multiple of 64): about 8 votes per lane, so the
-// lane's one inversion is shared, and at most the resident comb lanes
-uint32_t comb_sign_blocks(const DevCtx& d, uint64_t n) {
-  constexpr uint64_t per = 8;   // votes per lane
-  const uint64_t resident = (uint64_t)d.cus * d.comb_blocks_per_cu;
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, (n + 256 * per - 1) / (256 * per)));
-}
-int launch_comb_sign(DevCtx& d, const nwc::SignRecs& sr, uint64_t v0, uint64_t n, uint64_t* out_bits, hipStream_t s) {
-  if (n == 0) return 0;
-  if (v0 & 63) return set_err(NWC_ERR_ARG, "sign pass off a verdict word");
-  const uint32_t blocks = comb_sign_blocks(d, n);
-  hipLaunchKernelGGL(nwc::k_comb_sign, dim3(blocks), dim3(256), 0, s, sr, v0, n, out_bits);
-  HIP_TRY(hipGetLastError());
-  return 0;
-}
-
 // Device part of nwc_sanitize_messages: messages in HBM (ddata 4-byte aligned with >= 16 bytes
 // of readable padding, doff device u64[m+1] relative to ddata, `total` bytes), parsed as the
 // chunks cuts[k] .. cuts[k+1] (whole messages).  `chunk_ready(k)`, when given, returns once chunk
@@ -2543,11 +2632,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   // inversion per vote.  NWC_SIGN_DEFER=0: k_verify_comb per chunk (A/B).
   const bool chunked = nch > 1;
   const bool defer = chunked && deferrable_list(d);
-  static const bool sign_defer_on = [] {
-    const char* e = std::getenv("NWC_SIGN_DEFER");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  const bool ysplit = defer && sign_defer_on;
+  const bool ysplit = defer && sign_defer();
   const size_t need = align256(total + 128 * (m + 2)) + align256(32 * m) * 3 + align256(64 * m) + align256(32 * vt) +
                       align256(64 * vt) + align256(4 * vt) + align256(4) + align256(4 * m) + align256(16 * m) +
                       align256(4 * m) + align256(8 * ((m + 63) / 64)) + align256(8 * ((vt + 63) / 64)) +
@@ -2583,12 +2668,13 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   a.rec_n = c.take<uint32_t>(4 * m);
   uint64_t* sbits = c.take<uint64_t>(8 * ((m + 63) / 64));
   uint64_t* lbits = c.take<uint64_t>(8 * ((vt + 63) / 64));
-  nwc::SignRecs sr{};
+  nwc::SignRecs sr{};   // vote v's record at index v
   if (ysplit) {
     sr.x = c.take<uint32_t>(32 * vt);
     sr.z = c.take<uint32_t>(32 * vt);
     sr.p = c.take<uint32_t>(32 * vt);
     sr.meta = c.take<uint32_t>(4 * vt);
+    HIP_TRY(hipMemsetAsync(lbits, 0, 8 * ((vt + 63) / 64), s));   // the sign and list passes OR into it
   }
   a.digests = ddigests;
   if (vote_target) {
@@ -2646,10 +2732,11 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     }
     const uint64_t v0 = launched;
     const bool y = deferred && ysplit;
-    const nwc::SignPass sp{owed_lo, owed_hi - owed_lo, lbits, comb_sign_blocks(d, owed_hi - owed_lo)};
+    const nwc::SignPass sp{sr, owed_lo, owed_hi - owed_lo, lbits, comb_sign_blocks(d, owed_hi - owed_lo)};
+    const nwc::SignRecs srl = sign_recs_at(sr, (int64_t)v0);
     if (int rc = launch_verify(d, a.cdig, a.v_msg + v0, 0, a.v_pk + 32 * v0, a.v_sig + 64 * v0, upto - v0, 0,
                                lbits + v0 / 64, ls, deferred ? LV_DEFER_LIST : 0, nullptr, v0, nullptr,
-                               y ? &sr : nullptr, y ? &sp : nullptr))
+                               y ? &srl : nullptr, y ? &sp : nullptr))
       return rc;
     if (y) {
       owed_lo = v0;
@@ -2999,7 +3086,7 @@ int nwc_memory_info(nwc_memory* out) {
                                         (size_t)d.lk.cap * nwc::COMB_PER_KEY * sizeof(nwc::ge_niels_pad) +
                                         4 * (size_t)nwc::LK_SLOTS + 16
                                   : 0);
-    out->scratch = d.scratch_cap + d.straus_cap + d.msm_cap + d.rs_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap + d.pair_cap +
+    out->scratch = d.scratch_cap + d.straus_cap + d.msm_cap + d.rs_cap + d.arena_cap + d.msg_arena_cap + 12 * d.fb_cap + d.pair_cap + d.sign_cap +
                    8 * (size_t)d.ts_slot_count;
   }
   out->digesters = digester_device_bytes(d.hip_id);
@@ -3028,6 +3115,8 @@ int nwc_trim(void) {
   d.rs_buf = nullptr; d.rs_cap = 0;
   if (d.pair_buf) HIP_TRY(hipFree(d.pair_buf));
   d.pair_buf = nullptr; d.pair_cap = 0;
+  if (d.sign_buf) HIP_TRY(hipFree(d.sign_buf));
+  d.sign_buf = nullptr; d.sign_cap = 0;
   if (d.arena) HIP_TRY(hipFree(d.arena));
   if (d.msg_arena) HIP_TRY(hipFree(d.msg_arena));
   d.scratch = nullptr; d.scratch_cap = 0;
