@@ -1564,7 +1564,8 @@ __device__ __forceinline__ void comb_y_body(const VerifyArgs& a, const CombArgs&
     u32 mw[8], aw[8], sgw[16];
     load_inputs(a, active ? i : 0, mw, aw, sgw);
     const int key = committee_lookup(cm, aw);
-    if (active && key < 0) ca.list[atomicAdd(ca.count, 1u)] = ca.list_base + (uint32_t)i;
+    // (no list: the caller does not need uncached equations decided, their verdict stays 0)
+    if (active && key < 0 && ca.list) ca.list[atomicAdd(ca.count, 1u)] = ca.list_base + (uint32_t)i;
     const int kk = key < 0 ? 0 : key;
     u32 rw[8], sw[8];
     _Pragma("unroll") for (int q = 0; q < 8; ++q) { rw[q] = sgw[q]; sw[q] = sgw[8 + q]; }

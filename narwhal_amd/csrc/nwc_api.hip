@@ -1134,6 +1134,15 @@ bool sign_defer() {
   }();
   return on;
 }
+// NWC_STRICT_Y=0: the message pipeline's strict equations through launch_verify on the leaf
+// stream (A/B of the list-free strict launches on the parse stream)
+bool strict_y_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("NWC_STRICT_Y");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
 // Whether launch_verify takes the comb path (k_verify_comb) for a plain launch of n equations.
 bool takes_comb_path(const DevCtx& d, uint64_t n, int strict) {
   if (verify_path() != VPath::Default) return false;
@@ -2224,8 +2233,15 @@ static int batch_equation_many(const uint8_t* digests, const uint32_t* offsets, 
 std::mutex g_cm_mu;
 static int set_committee_locked(const uint8_t* pks, size_t n);
 
+// The committee cache holds exactly nwc_set_committee_config's committee (set there, cleared by
+// nwc_set_committee): the message pipeline may then leave the strict equations of uncached keys
+// undecided -- their authors are outside the committee, and UnknownAuthority precedes
+// InvalidSignature for every message kind (primary/src/core.rs, messages.rs).
+std::atomic<bool> g_cm_is_config{false};
+
 int nwc_set_committee(const uint8_t* pks, size_t n) {
   std::lock_guard<std::mutex> lk(g_cm_mu);
+  g_cm_is_config = false;
   return set_committee_locked(pks, n);
 }
 
@@ -2574,7 +2590,9 @@ int nwc_set_committee_config(const uint8_t* pks, const uint64_t* stakes, size_t 
   worker_offsets = uoff.data();
   worker_ids = uids.data();
   std::lock_guard<std::mutex> cm_lk(g_cm_mu);
+  g_cm_is_config = false;
   if (int rc = set_committee_locked(pks, n)) return rc;
+  g_cm_is_config = true;
   uint64_t total = 0;
   for (size_t k = 0; k < n; ++k) total += stakes[k];
   for (auto& dp : g_devs) {
@@ -2636,7 +2654,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   const size_t need = align256(total + 128 * (m + 2)) + align256(32 * m) * 3 + align256(64 * m) + align256(32 * vt) +
                       align256(64 * vt) + align256(4 * vt) + align256(4) + align256(4 * m) + align256(16 * m) +
                       align256(4 * m) + align256(8 * ((m + 63) / 64)) + align256(8 * ((vt + 63) / 64)) +
-                      (ysplit ? 3 * align256(32 * vt) + align256(4 * vt) : 0);
+                      (ysplit ? 3 * align256(32 * vt) + align256(4 * vt) + 3 * align256(32 * m) + align256(4 * m) : 0);
   if (need > d.msg_arena_cap) {
     HIP_TRY(hipEventSynchronize(d.scratch_free));
     HIP_TRY(hipStreamSynchronize(s));
@@ -2675,6 +2693,14 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
     sr.p = c.take<uint32_t>(32 * vt);
     sr.meta = c.take<uint32_t>(4 * vt);
     HIP_TRY(hipMemsetAsync(lbits, 0, 8 * ((vt + 63) / 64), s));   // the sign and list passes OR into it
+  }
+  nwc::SignRecs srs{};   // the strict equations' records (message i at index i)
+  if (ysplit) {
+    srs.x = c.take<uint32_t>(32 * m);
+    srs.z = c.take<uint32_t>(32 * m);
+    srs.p = c.take<uint32_t>(32 * m);
+    srs.meta = c.take<uint32_t>(4 * m);
+    HIP_TRY(hipMemsetAsync(sbits, 0, 8 * ((m + 63) / 64), s));
   }
   a.digests = ddigests;
   if (vote_target) {
@@ -2760,8 +2786,23 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   };
   // the strict equations (headers' and votes' own signatures) of messages [c0, c1) on the leaf
   // stream, after the list passes (the strict launch reuses the list)
+  // With the cache holding exactly the configured committee (g_cm_is_config) and the sign tests
+  // deferred, strict equations [c0, c1) go on the parse stream as k_verify_comb_y without a list
+  // (an uncached key is a non-member: UnknownAuthority decides first) and their sign pass, off the
+  // leaf stream, which then carries only the leaves and their list passes.
+  bool strict_y = false;   // set below once the cuts are known to be aligned
   auto strict = [&](size_t c0, size_t c1) -> int {
     if (c1 <= c0) return 0;
+    if (strict_y) {
+      const uint64_t n = c1 - c0;
+      const nwc::VerifyArgs va{a.eq_msg + 32 * c0, nullptr, 1, a.eq_pk + 32 * c0, a.eq_sig + 64 * c0, sbits + c0 / 64,
+                               n, 1, d.base_table, d.base24, d.scratch, d.fb_list, d.fb_count, 0u, cm};
+      const nwc::CombArgs ca{nullptr, nullptr, d.comb_base, d.comb16, nullptr, 0};
+      const unsigned gy = (unsigned)std::min<uint64_t>((n + 255) / 256, 60000);
+      hipLaunchKernelGGL(nwc::k_verify_comb_y, dim3(gy), dim3(256), 0, s, va, ca, sign_recs_at(srs, (int64_t)c0));
+      HIP_TRY(hipGetLastError());
+      return launch_comb_sign(d, srs, c0, n, sbits, s);
+    }
     if (int rc = finish()) return rc;
     list_dirty = true;
     return launch_verify(d, a.eq_msg + 32 * c0, nullptr, 1, a.eq_pk + 32 * c0, a.eq_sig + 64 * c0, c1 - c0, 1,
@@ -2775,6 +2816,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
   bool aligned = true;
   for (size_t k = 1; k < nch; ++k) aligned = aligned && (cuts[k] & 63) == 0;
   const size_t strict_at = aligned && nch >= 3 ? nch / 3 : (nch >= 2 ? nch - 2 : 0);   // its iteration k
+  strict_y = ysplit && aligned && g_cm_is_config.load() && strict_y_on();
   size_t strict_done = 0;   // messages [0, strict_done) have their strict launch queued
   uint64_t nv = 0;
   size_t queued = 0;   // chunks whose parse is queued
@@ -2845,6 +2887,7 @@ static int sanitize_dev(DevCtx& d, const uint8_t* ddata, const uint64_t* doff, s
       // their sign tests, then the list passes and the remaining strict equations
       if (int rc = leaves(nv, true)) return rc;
       if (int rc = strict(strict_done, m)) return rc;
+      if (int rc = finish()) return rc;   // (strict_y: the strict launches left the leaf stream's passes)
     } else {
       if (int rc = strict(strict_done, m)) return rc;
       if (int rc = leaves(nv, false)) return rc;

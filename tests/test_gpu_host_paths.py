@@ -167,13 +167,15 @@ def test_sanitize_messages_host_staged():
     _sanitize_tiled_golden()
 
 
-@pytest.mark.parametrize("sign_defer", ["1", "0"])
-def test_sanitize_messages_host_chunks(sign_defer):
+@pytest.mark.parametrize("env", [{}, {"NWC_SIGN_DEFER": "0"}, {"NWC_STRICT_Y": "0"}])
+def test_sanitize_messages_host_chunks(env):
     """The same batch in 1-MB pipelined chunks (NWC_MSG_CHUNK, read once per process: a child
     process) -- the production pipeline forced to ~8 chunks cut on 64-message boundaries, sharing
     one 64-aligned vote counter, each parsed while the previous one's leaves run on the side stream,
     with the leaves' sign tests deferred (k_verify_comb_y / k_verify_comb_y_sign / k_comb_sign) or
-    decided in k_verify_comb (NWC_SIGN_DEFER=0) -- codes and digests unchanged.  (Round 6 removed
+    decided in k_verify_comb (NWC_SIGN_DEFER=0), and the strict equations list-free on the parse
+    stream (the default: an uncached author is a non-member, UnknownAuthority first) or through
+    the comb path's lists on the leaf stream (NWC_STRICT_Y=0) -- codes and digests unchanged.  (Round 6 removed
     the pipeline's A/B switches that lost or tied: profiles/r05/wire_host.md.)"""
     import os
     import subprocess
@@ -184,8 +186,7 @@ def test_sanitize_messages_host_chunks(sign_defer):
             "_sanitize_tiled_golden()\n"
             "print('done', flush=True)\n" % ROOT)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=ROOT,
-                       env=dict(os.environ, NWC_MSG_CHUNK=str(1 << 20), NWC_HOST_TIMING="1",
-                                NWC_SIGN_DEFER=sign_defer))
+                       env=dict(os.environ, NWC_MSG_CHUNK=str(1 << 20), NWC_HOST_TIMING="1", **env))
     assert r.returncode == 0 and "done" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-3000:])
     steps = [l for l in r.stderr.splitlines() if l.startswith("nwc sanitize steps:")]
     assert steps and all(l.count("parse queued") >= 4 for l in steps), r.stderr[-2000:]   # several chunks
