@@ -284,3 +284,41 @@ def test_large_unsorted_headers(lib, oracle):
         assert dt < 2.0, dt
     finally:
         lib.nwc_set_committee(None, 0)
+
+
+@pytest.mark.parametrize("env", [{}, {"NWC_STRICT_Y": "0"}, {"NWC_SIGN_DEFER": "0"}])
+def test_random_batches_chunked_vs_oracle(oracle, tmp_path, env):
+    """The random batch (outsiders, bad header and vote signatures, quorum failures, base64 key
+    forms, truncations) tiled to ~10 MB and sent through the chunked host pipeline in 1-MB chunks
+    (a child process: libnwc reads NWC_MSG_CHUNK once): every code and digest equals the
+    restatement's.  Covers the strict equations without the uncached list on the parse stream
+    (outsiders' messages end in UnknownAuthority first), the list path and k_verify_comb."""
+    import subprocess
+    import messages_ref as mr
+    rng = np.random.default_rng(2026)
+    committee, pks, stakes, workers, msgs = _random_batch(oracle, rng)
+    sig = _CSig(oracle)
+    exp = [mr.sanitize(m, committee, sig, 0) for m in msgs]
+    reps = 1 + (10 << 20) // sum(len(m) for m in msgs)
+    tiled = msgs * reps
+    offs = np.zeros(len(tiled) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in tiled])
+    woffs, wids = [0], []
+    for w in workers:
+        wids.extend(w)
+        woffs.append(len(wids))
+    inp, out = str(tmp_path / "in.npz"), str(tmp_path / "out.npz")
+    np.savez(inp, data=np.frombuffer(b"".join(tiled), np.uint8), offs=offs,
+             keys=np.frombuffer(b"".join(pks), np.uint8).reshape(len(pks), 32), stakes=np.array(stakes, np.uint64),
+             woffs=np.array(woffs, np.uint32), wids=np.array(wids, np.uint32), gc=0)
+    e = dict(os.environ, NWC_MSG_CHUNK=str(1 << 20), **env)
+    subprocess.run([sys.executable, os.path.join(ROOT, "tests", "sanitize_chunk_helper.py"), inp, out, ROOT], env=e,
+                   check=True, timeout=300)
+    r = np.load(out)
+    for i in range(len(tiled)):
+        code, kind, d = exp[i % len(msgs)]
+        assert r["codes"][i] == code, (env, i, int(r["codes"][i]), mr.NAMES[code])
+        if kind in (0, 1, 2):
+            assert r["dig"][i].tobytes() == d, (env, i)
+    counts = np.bincount(r["codes"], minlength=12)
+    assert counts[0] > 100 and counts[1] > 5 and counts[4] > 5
